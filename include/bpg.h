@@ -1,0 +1,187 @@
+/*
+ * bpg.h — C ABI of the MI355X-native Bulletproofs R1CS prover/verifier
+ * (drop-in for FairAds/bulletproof-gadgets @ 2025-02-02).
+ *
+ * Two layers are exported by libbpg.so:
+ *
+ *  1. The UPWARD drop-in ABI (what the reference's FFI binds):
+ *       c_prove / c_verify / free_proof  — interfaces/ios/src/lib.rs:10-66,
+ *       header interfaces/ios/src/bulletproofs_ios.h:4-13.
+ *     Behaviour follows src/prove.rs:37-82 and src/verify.rs:36-73 (statement
+ *     text in, `.coms` text + `.proof` bytes out). The reference panics on bad
+ *     input (UB across `extern fn`); here errors return NULL / false and the
+ *     reason is available from bpg_last_error().
+ *     NOTE: the reference header declares `int proof_len` but the Rust struct
+ *     uses `usize`; this header uses size_t (what the Rust side really passes).
+ *
+ *  2. The INNER operator ABI at the hot-path cut (`Prover::prove`,
+ *     src/prove.rs:79, and `Verifier::verify`, src/verify.rs:71): a flattened
+ *     constraint system (bpg_r1cs_view) goes in, proof bytes come out. The
+ *     transcript and RNG stay on the host, all group arithmetic (MSM, IPP
+ *     folding, commitments, point (de)compression) and the bulk scalar-vector
+ *     work run in HIP kernels on gfx950.
+ *
+ * All scalars cross the ABI as 32-byte little-endian strings, all points as
+ * 32-byte compressed Ristretto255 encodings. Every entry point returns a
+ * status (>= 0 success, < 0 error) and never throws across the boundary.
+ */
+#ifndef BPG_H
+#define BPG_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdbool.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* 1. Upward drop-in ABI (interfaces/ios/src/lib.rs:10-66)                   */
+/* ------------------------------------------------------------------------ */
+
+/* interfaces/ios/src/lib.rs:10-18 (#[repr(C)] struct ProofArtifacts). */
+struct ProofArtifacts {
+    const char *commitments;   /* NUL-terminated `.coms` text            */
+    const uint8_t *proof;      /* proof bytes (417 + 64*lg(N))           */
+    size_t proof_len;
+    size_t proof_cap;
+};
+
+/* interfaces/ios/src/lib.rs:20-42 -> src/prove.rs:37 `prove`.
+ * Returns NULL on any error (bpg_last_error() tells why). */
+struct ProofArtifacts *c_prove(const char *name, const char *instance,
+                               const char *witness, const char *gadgets);
+
+/* interfaces/ios/src/lib.rs:44-52 -> src/verify.rs:36 `verify`.
+ * true iff the proof verifies; false on rejection or on any error. */
+bool c_verify(const char *name, const char *instance, const char *gadgets,
+              const char *commitments, const uint8_t *proof, size_t proof_len);
+
+/* interfaces/ios/src/lib.rs:54-66. Accepts NULL. */
+void free_proof(struct ProofArtifacts *artifacts);
+
+/* Added: thread-local description of the last error ("" if none). */
+const char *bpg_last_error(void);
+
+/* Added: deterministic mode. Every `thread_rng()` draw of the reference
+ * (commitment blindings gadget.rs:32, commitments.rs:28,40 and the 32-byte
+ * TranscriptRng finalize entropy inside Prover::prove / Verifier::verify)
+ * comes from one ChaCha20 stream keyed by `seed`, consumed in program order.
+ * Applies to calls made on the calling thread after this call.
+ * bpg_clear_seed() returns to OS entropy. */
+void bpg_set_seed(uint64_t seed);
+void bpg_clear_seed(void);
+
+/* Added: select the HIP device used by the calling thread (default 0). */
+int bpg_set_device(int device);
+
+/* ------------------------------------------------------------------------ */
+/* 2. Inner operator ABI: the flattened constraint system                     */
+/* ------------------------------------------------------------------------ */
+
+/* Variable encoding inside a linear-combination term (bulletproofs r1cs
+ * `Variable`): kind in the top 4 bits, index in the low 28 bits. */
+#define BPG_VAR_ONE 0u        /* Variable::One()                      */
+#define BPG_VAR_L 1u          /* Variable::MultiplierLeft(i)          */
+#define BPG_VAR_R 2u          /* Variable::MultiplierRight(i)         */
+#define BPG_VAR_O 3u          /* Variable::MultiplierOutput(i)        */
+#define BPG_VAR_V 4u          /* Variable::Committed(i)               */
+#define BPG_VAR(kind, idx) (((uint32_t)(kind) << 28) | ((uint32_t)(idx) & 0x0FFFFFFFu))
+#define BPG_VAR_KIND(v) ((uint32_t)(v) >> 28)
+#define BPG_VAR_INDEX(v) ((uint32_t)(v) & 0x0FFFFFFFu)
+
+/* The state `Prover::prove` consumes (bulletproofs r1cs::Prover fields
+ * `secrets {a_L,a_R,a_O,v,v_blinding}` and `constraints`). The verifier side
+ * uses the same struct with the secret arrays set to NULL. */
+typedef struct bpg_r1cs_view {
+    uint32_t n;               /* multiplication gates (a_L.len())        */
+    uint32_t m;               /* high-level commitments (v.len())         */
+    uint32_t q;               /* linear constraints (constraints.len())  */
+    uint32_t nnz;             /* total terms over all constraints        */
+    const uint8_t *a_L;       /* n x 32 (prover only)                    */
+    const uint8_t *a_R;       /* n x 32 (prover only)                    */
+    const uint8_t *a_O;       /* n x 32 (prover only)                    */
+    const uint8_t *v;         /* m x 32 raw scalars (prover only; may be
+                                 non-canonical, Scalar::from_bits)        */
+    const uint8_t *v_blinding;/* m x 32 (prover only)                    */
+    const uint32_t *row_ptr;  /* q + 1 offsets into the term arrays      */
+    const uint32_t *term_var; /* nnz encoded variables                   */
+    const uint8_t *term_coeff;/* nnz x 32 coefficients (raw scalars)     */
+} bpg_r1cs_view;
+
+/* Maximum proof length for lg(N) <= 31: 417 + 64*31. */
+#define BPG_MAX_PROOF_LEN (417u + 64u * 31u)
+
+/* Opaque device context: owns the HBM-resident generator cache
+ * (BulletproofGens::new, prove.rs:78) and per-call streams/workspaces. */
+typedef struct bpg_ctx bpg_ctx;
+
+bpg_ctx *bpg_ctx_create(int device);
+void bpg_ctx_destroy(bpg_ctx *ctx);
+
+/* Ensure G_i, H_i for i < capacity are resident (BulletproofGens::new(cap,1),
+ * bulletproofs@2.1.0 generators.rs). */
+int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity);
+
+/* Pedersen commitments V_i = v_i*B + vb_i*B_blinding (PedersenGens::commit,
+ * used by Prover::commit at commitments.rs:28,40 and gadget.rs:32). */
+int bpg_pedersen_commit(bpg_ctx *ctx, const uint8_t *v, const uint8_t *vb,
+                        uint32_t count, uint8_t *V_out);
+
+/* Hot path: bulletproofs r1cs::Prover::prove (prove.rs:79) for a one-phase
+ * circuit, preceded by the transcript prefix Transcript::new(label),
+ * r1cs_domain_sep and one append_point("V") per commitment (V computed on
+ * device from v/v_blinding and returned in V_out, m x 32).
+ * `entropy` is the 32-byte input of TranscriptRngBuilder::finalize.
+ * Writes proof bytes (R1CSProof::to_bytes, prove.rs:81). */
+int bpg_r1cs_prove(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
+                   const bpg_r1cs_view *cs, const uint8_t entropy[32],
+                   uint8_t *proof_out, size_t proof_cap, size_t *proof_len,
+                   uint8_t *V_out);
+
+/* Hot path: bulletproofs r1cs::Verifier::verify (verify.rs:71). `V` holds
+ * the m compressed commitments in commit order. Returns 1 = accept,
+ * 0 = reject, < 0 = error. */
+int bpg_r1cs_verify(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
+                    const bpg_r1cs_view *cs, const uint8_t *V,
+                    const uint8_t *proof, size_t proof_len,
+                    const uint8_t entropy[32]);
+
+/* Prepared (HBM-resident) circuit for repeated proving: uploads a_L/a_R/a_O
+ * and the transposed constraint matrix once. */
+typedef struct bpg_prepared bpg_prepared;
+bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs);
+void bpg_prepared_free(bpg_prepared *p);
+
+/* Prove `count` independent proofs of one prepared circuit (proof k uses
+ * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
+ * host threads sharing the device. lens[k] receives each proof length. */
+int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len,
+                    const uint8_t *entropy, uint32_t count, uint32_t threads,
+                    uint8_t *proof_out, size_t proof_stride, size_t *lens);
+
+/* Per-phase wall-clock timers of the last prove on this thread (ms):
+ * [0] transcript+rng, [1] commit MSMs, [2] vectors, [3] IPP, [4] total. */
+int bpg_last_timings(double *out, int n);
+
+/* Generic device MSM: out = sum scalars[i] * points[i] (compressed in/out).
+ * Test hook for the Pippenger kernel. Returns <0 if a point fails to
+ * decompress. */
+int bpg_msm(bpg_ctx *ctx, const uint8_t *scalars, const uint8_t *points,
+            uint32_t count, uint8_t out[32]);
+
+/* Statement synthesis only (no proof): runs the prover-side driver of
+ * prove.rs:37-75 under the current seed and exports the flattened system.
+ * Buffers are owned by the returned handle. */
+typedef struct bpg_synth bpg_synth;
+bpg_synth *bpg_synthesize(const char *instance, const char *witness,
+                          const char *gadgets);
+const bpg_r1cs_view *bpg_synth_view(const bpg_synth *s);
+const char *bpg_synth_commitments(const bpg_synth *s);
+void bpg_synth_free(bpg_synth *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPG_H */
