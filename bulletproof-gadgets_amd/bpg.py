@@ -1,0 +1,252 @@
+"""Python host binding of libbpg.so (ctypes over include/bpg.h).
+
+Mirrors the reference's entry points for tests and the benchmark:
+  prove(name, instance, witness, gadgets) -> (proof bytes, .coms text)
+      src/prove.rs:37 `prove` through the iOS C-ABI c_prove
+      (interfaces/ios/src/lib.rs:20-42)
+  verify(name, instance, proof, commitments, gadgets) -> bool
+      src/verify.rs:36 `verify` through c_verify (lib.rs:44-52)
+Errors raise BpgError (the reference panics); the library itself never
+falls back to a CPU path: without a HIP device every proving/verifying call
+fails with "no HIP device available".
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbpg.so")
+MAX_PROOF = 417 + 64 * 31
+
+# every symbol include/bpg.h declares
+EXPORTS = [
+    "c_prove", "c_verify", "free_proof", "bpg_last_error", "bpg_last_num_constraints", "bpg_set_seed",
+    "bpg_clear_seed", "bpg_set_device", "bpg_ctx_create", "bpg_ctx_destroy", "bpg_gens_ensure",
+    "bpg_pedersen_commit", "bpg_r1cs_prove", "bpg_r1cs_verify", "bpg_prepare", "bpg_prepared_free",
+    "bpg_prove_batch", "bpg_last_timings", "bpg_msm", "bpg_synthesize", "bpg_synthesize_verifier",
+    "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free",
+]
+
+
+class BpgError(RuntimeError):
+    pass
+
+
+class ProofArtifacts(ctypes.Structure):
+    _fields_ = [("commitments", ctypes.c_char_p), ("proof", ctypes.POINTER(ctypes.c_uint8)),
+                ("proof_len", ctypes.c_size_t), ("proof_cap", ctypes.c_size_t)]
+
+
+class R1csView(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32), ("m", ctypes.c_uint32), ("q", ctypes.c_uint32), ("nnz", ctypes.c_uint32),
+        ("a_L", ctypes.c_void_p), ("a_R", ctypes.c_void_p), ("a_O", ctypes.c_void_p),
+        ("v", ctypes.c_void_p), ("v_blinding", ctypes.c_void_p),
+        ("row_ptr", ctypes.c_void_p), ("term_var", ctypes.c_void_p), ("term_coeff", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BpgError("libbpg.so is not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, u32, u64, cp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p
+        L.c_prove.restype = ctypes.POINTER(ProofArtifacts)
+        L.c_prove.argtypes = [cp, cp, cp, cp]
+        L.c_verify.restype = ctypes.c_bool
+        L.c_verify.argtypes = [cp, cp, cp, cp, vp, sz]
+        L.free_proof.argtypes = [ctypes.POINTER(ProofArtifacts)]
+        L.bpg_last_error.restype = cp
+        L.bpg_last_num_constraints.restype = u64
+        L.bpg_set_seed.argtypes = [u64]
+        L.bpg_set_device.argtypes = [ctypes.c_int]
+        L.bpg_ctx_create.restype = vp
+        L.bpg_ctx_create.argtypes = [ctypes.c_int]
+        L.bpg_ctx_destroy.argtypes = [vp]
+        L.bpg_gens_ensure.argtypes = [vp, u32]
+        L.bpg_pedersen_commit.argtypes = [vp, vp, vp, u32, vp]
+        L.bpg_r1cs_prove.argtypes = [vp, vp, sz, ctypes.POINTER(R1csView), vp, vp, sz, ctypes.POINTER(sz), vp]
+        L.bpg_r1cs_verify.argtypes = [vp, vp, sz, ctypes.POINTER(R1csView), vp, vp, sz, vp]
+        L.bpg_prepare.restype = vp
+        L.bpg_prepare.argtypes = [vp, ctypes.POINTER(R1csView)]
+        L.bpg_prepared_free.argtypes = [vp]
+        L.bpg_prove_batch.argtypes = [vp, vp, sz, vp, u32, u32, vp, sz, ctypes.POINTER(sz)]
+        L.bpg_last_timings.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.bpg_msm.argtypes = [vp, vp, vp, u32, vp]
+        L.bpg_synthesize.restype = vp
+        L.bpg_synthesize.argtypes = [cp, cp, cp]
+        L.bpg_synthesize_verifier.restype = vp
+        L.bpg_synthesize_verifier.argtypes = [cp, cp, cp]
+        L.bpg_synth_view.restype = ctypes.POINTER(R1csView)
+        L.bpg_synth_view.argtypes = [vp]
+        L.bpg_synth_commitments.restype = cp
+        L.bpg_synth_commitments.argtypes = [vp]
+        L.bpg_synth_V.restype = vp
+        L.bpg_synth_V.argtypes = [vp]
+        L.bpg_synth_free.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().bpg_last_error().decode(errors="replace")
+
+
+def set_seed(seed):
+    lib().bpg_set_seed(seed)
+
+
+def clear_seed():
+    lib().bpg_clear_seed()
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else s
+
+
+def prove(name, instance, witness, gadgets):
+    """prove.rs:37 -> (proof bytes, commitments text)."""
+    a = lib().c_prove(_b(name), _b(instance), _b(witness), _b(gadgets))
+    if not a:
+        raise BpgError(last_error())
+    try:
+        proof = bytes(a.contents.proof[:a.contents.proof_len])
+        coms = a.contents.commitments.decode()
+    finally:
+        lib().free_proof(a)
+    return proof, coms
+
+
+def verify(name, instance, proof, commitments, gadgets):
+    """verify.rs:36 -> bool (False also on malformed input; see last_error())."""
+    return bool(lib().c_verify(_b(name), _b(instance), _b(gadgets), _b(commitments), proof, len(proof)))
+
+
+def num_constraints():
+    return lib().bpg_last_num_constraints()
+
+
+class Synth:
+    """Statement synthesis without device work (flattened system export)."""
+
+    def __init__(self, instance, witness=None, gadgets="", commitments=None):
+        if commitments is None:
+            h = lib().bpg_synthesize(_b(instance), _b(witness), _b(gadgets))
+        else:
+            h = lib().bpg_synthesize_verifier(_b(instance), _b(commitments), _b(gadgets))
+        if not h:
+            raise BpgError(last_error())
+        self.h = h
+        self.prover = commitments is None
+        v = lib().bpg_synth_view(h).contents
+        self.n, self.m, self.q, self.nnz = v.n, v.m, v.q, v.nnz
+        self.view = v
+
+    def names(self):
+        return [l for l in lib().bpg_synth_commitments(self.h).decode().splitlines() if l]
+
+    def vec(self, field, count):
+        p = getattr(self.view, field)
+        raw = ctypes.string_at(p, 32 * count) if count else b""
+        return [raw[32 * i:32 * i + 32] for i in range(count)]
+
+    def rows(self):
+        v = self.view
+        rp = (ctypes.c_uint32 * (self.q + 1)).from_address(v.row_ptr)
+        tv = (ctypes.c_uint32 * max(self.nnz, 1)).from_address(v.term_var)
+        tc = ctypes.string_at(v.term_coeff, 32 * self.nnz) if self.nnz else b""
+        out = []
+        for r in range(self.q):
+            out.append([(tv[k], tc[32 * k:32 * k + 32]) for k in range(rp[r], rp[r + 1])])
+        return out
+
+    def V(self):
+        return ctypes.string_at(lib().bpg_synth_V(self.h), 32 * self.m) if self.m else b""
+
+    def __del__(self):
+        try:
+            lib().bpg_synth_free(self.h)
+        except Exception:
+            pass
+
+
+class Context:
+    """Device context (generator cache in HBM) for the inner ABI."""
+
+    def __init__(self, device=0):
+        self.h = lib().bpg_ctx_create(device)
+        if not self.h:
+            raise BpgError(last_error())
+
+    def msm(self, scalars, points):
+        out = ctypes.create_string_buffer(32)
+        rc = lib().bpg_msm(self.h, b"".join(scalars), b"".join(points), len(scalars), out)
+        if rc != 0:
+            raise BpgError("bpg_msm failed (%d): %s" % (rc, last_error()))
+        return out.raw
+
+    def pedersen(self, v, vb):
+        out = ctypes.create_string_buffer(32 * max(len(v), 1))
+        if lib().bpg_pedersen_commit(self.h, b"".join(v), b"".join(vb), len(v), out) != 0:
+            raise BpgError(last_error())
+        return [out.raw[32 * i:32 * i + 32] for i in range(len(v))]
+
+    def r1cs_prove(self, label, view, entropy):
+        out = ctypes.create_string_buffer(MAX_PROOF)
+        plen = ctypes.c_size_t(0)
+        V = ctypes.create_string_buffer(32 * max(view.m, 1))
+        rc = lib().bpg_r1cs_prove(self.h, label, len(label), ctypes.byref(view), entropy, out, MAX_PROOF,
+                                  ctypes.byref(plen), V)
+        if rc != 0:
+            raise BpgError(last_error())
+        return out.raw[:plen.value], [V.raw[32 * i:32 * i + 32] for i in range(view.m)]
+
+    def r1cs_verify(self, label, view, V, proof, entropy=b"\x05" * 32):
+        Vb = b"".join(V) or b"\0" * 32
+        rc = lib().bpg_r1cs_verify(self.h, label, len(label), ctypes.byref(view), Vb, proof, len(proof), entropy)
+        if rc < 0:
+            raise BpgError(last_error())
+        return rc == 1
+
+    def prepare(self, view):
+        p = lib().bpg_prepare(self.h, ctypes.byref(view))
+        if not p:
+            raise BpgError(last_error())
+        return Prepared(p)
+
+    def __del__(self):
+        try:
+            lib().bpg_ctx_destroy(self.h)
+        except Exception:
+            pass
+
+
+class Prepared:
+    def __init__(self, h):
+        self.h = h
+
+    def prove_batch(self, label, entropies, threads):
+        count = len(entropies)
+        stride = MAX_PROOF
+        out = ctypes.create_string_buffer(stride * max(count, 1))
+        lens = (ctypes.c_size_t * max(count, 1))()
+        rc = lib().bpg_prove_batch(self.h, label, len(label), b"".join(entropies), count, threads, out, stride, lens)
+        if rc != 0:
+            raise BpgError(last_error())
+        return [out.raw[stride * k:stride * k + lens[k]] for k in range(count)]
+
+    def __del__(self):
+        try:
+            lib().bpg_prepared_free(self.h)
+        except Exception:
+            pass
+
+
+def last_timings():
+    arr = (ctypes.c_double * 5)()
+    lib().bpg_last_timings(arr, 5)
+    return {"rng_ms": arr[0], "commit_ms": arr[1], "vec_ms": arr[2], "ipp_ms": arr[3], "total_ms": arr[4]}

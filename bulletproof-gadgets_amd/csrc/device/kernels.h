@@ -1,0 +1,127 @@
+// kernels.h — host-callable launch wrappers for the gfx950 kernels of the
+// Bulletproofs R1CS hot path (bulletproofs@2.1.0 Prover::prove /
+// Verifier::verify, InnerProductProof::create). Only plain pointers cross this
+// boundary; device buffers are owned by the caller (Workspace / Context).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bpg {
+namespace dev {
+
+// Device layouts (must match dev_field.h): 32 B scalars / field elements,
+// 128 B extended points (X, Y, Z, T).
+struct ScD { uint32_t v[8]; };
+struct PtD { uint32_t v[32]; };
+
+#define BPG_HIP(x)                                                                 \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) throw ::bpg::dev::HipError(e_, #x, __FILE__, __LINE__); \
+    } while (0)
+
+struct HipError {
+    hipError_t err;
+    const char *expr, *file;
+    int line;
+    HipError(hipError_t e, const char *x, const char *f, int l) : err(e), expr(x), file(f), line(l) {}
+};
+
+// -------------------------------------------------------------- points
+// out[i] = from_uniform_bytes(uniform[64*i .. 64*i+64))
+void launch_gens_map(const uint8_t *uniform, PtD *out, uint32_t count, hipStream_t st);
+// out[i] = v[i]*B + vb[i]*B_blinding using fixed-base tables (64 x 8 points each)
+void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tabB, const PtD *tabBb,
+                     uint32_t *out_compressed, hipStream_t st);
+void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st);
+void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hipStream_t st);
+
+// -------------------------------------------------------------- MSM
+struct MsmSeg {
+    const ScD *scal;   // canonical scalars (< l)
+    const PtD *base;   // extended points
+    uint32_t count;
+    uint32_t msm;      // which MSM of the job this segment contributes to
+};
+struct MsmPlan {
+    int c, W, nmsm, rows, half;
+    uint64_t total;         // points in the job
+    uint64_t E0;            // W * total
+    uint32_t T;             // chunk size of the reduce-by-key passes
+    int passes;
+    uint64_t capE;          // capacity after the first pass
+    uint32_t key_bits;
+    size_t sort_tmp, scan_tmp;
+    int nseg_per_row, seglen;
+};
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void grow(size_t need);
+};
+class MsmEngine {
+  public:
+    explicit MsmEngine(hipStream_t st) : st_(st) {}
+    ~MsmEngine();
+    // Enqueue a multi-MSM job on the stream; window-row sums land in
+    // `rows_host` (pinned, nmsm * W points) when `done` fires.
+    // Returns the plan (window width c and count W are needed by the host
+    // combine). Segments: at most 8.
+    MsmPlan enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host);
+  private:
+    void reserve(const MsmPlan &p);
+    hipStream_t st_;
+    DBuf keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_, cnt_, off_, E_, rk_a_, rk_b_, rp_a_, rp_b_, buckets_,
+        segacc_, rows_dev_;
+};
+
+// -------------------------------------------------------------- scalar vectors
+// out[i] = base^(start + i) for i < count, given base2[b] = base^(2^b), b < 32
+void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out, hipStream_t st);
+// out[i] = lo[i & 1023] * hi[i >> 10]
+void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD *out, hipStream_t st);
+// flattened_constraints: columns in CSC form; out[col] = sgn * sum coeff * z^(q+1)
+struct CscDev {
+    const uint32_t *col_ptr;   // ncol + 1
+    const uint32_t *row;       // nnz, constraint index q
+    const ScD *coeff;          // nnz, canonical
+    const uint32_t *short_cols, *long_cols;  // column ids by length class
+    uint32_t nshort, nlong, ncol;
+    uint32_t neg_from;         // columns >= neg_from are negated (V and One)
+};
+void launch_flatten(const CscDev &csc, const ScD *zlo, const ScD *zhi, ScD *out, hipStream_t st);
+// l(x)/r(x) coefficient vectors (VecPoly3, prover.rs)
+void launch_lr_build(const ScD *aL, const ScD *aR, const ScD *sR, const ScD *wL, const ScD *wR,
+                     const ScD *wO, const ScD *yp, const ScD *yip, uint32_t n, ScD *l1, ScD *r0, ScD *r1,
+                     ScD *r3, hipStream_t st);
+// t1..t6 of special_inner_product -> out[6]; partial is scratch (>= 6 * 1024)
+void launch_tpoly(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, const ScD *r1, const ScD *r3,
+                  uint32_t n, ScD *partial, ScD *out6, hipStream_t st);
+// out = sum a[i] * b[i] (i < n)
+void launch_dot(const ScD *a, const ScD *b, uint32_t n, ScD *partial, ScD *out, hipStream_t st);
+// l_vec, r_vec at x (padded to N; r_vec[i] = -y^i for i >= n)
+// xm, x2m: x and x^2 in Montgomery form (x * 2^256 mod l)
+void launch_lr_eval(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, const ScD *r1, const ScD *r3,
+                    const ScD *yp, uint32_t n, uint32_t N, ScD xm, ScD x2m, ScD *a, ScD *b, hipStream_t st);
+
+// -------------------------------------------------------------- IPP
+struct IppRoundArgs {
+    uint32_t h, n;            // half length, number of real gates
+    ScD lamG1, lamGu;         // lambda_k * Gf[i] for i < n / i >= n
+    ScD muH1, muHu;           // mu_k * Gf[i] for i < n / i >= n  (times y^-i in-kernel)
+};
+// msm_scal[0..4h) = [aL*lamGf_R | bR*muHf_L | aR*lamGf_L | bL*muHf_R]; c_L -> msm_scal[4h],
+// c_R -> msm_scal[4h+1]
+void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
+                     ScD *partial, hipStream_t st);
+void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st);
+// Ghat' = Ghat_L + rho * Ghat_R (rho = rho_a except lanes i < n <= h+i, which use rho_b)
+void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
+                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, hipStream_t st);
+// verifier helpers
+void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
+                      ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st);
+void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st);
+
+}  // namespace dev
+}  // namespace bpg

@@ -1,0 +1,846 @@
+// kernels.hip — gfx950 kernels for the Bulletproofs R1CS hot path.
+//
+// Reference semantics (un-vendored crates pinned in Cargo.lock):
+//   bulletproofs@2.1.0  r1cs/prover.rs Prover::prove, r1cs/verifier.rs,
+//                       inner_product_proof.rs InnerProductProof::create,
+//                       generators.rs BulletproofGens/PedersenGens
+//   curve25519-dalek@3.2.0  Straus/Pippenger MSM, Ristretto encode/decode
+// Design (MI355X-first, not a port): one thread per point/scalar lane,
+// 64-wide waves, sort-based signed-window Pippenger (hipcub radix sort +
+// fixed-chunk reduce-by-key passes, no 128-byte atomics), Montgomery scalar
+// vectors, and a weighted single-scalar IPP point fold.
+#include <hipcub/hipcub.hpp>
+
+#include "dev_field.h"
+#include "kernels.h"
+
+namespace bpg {
+namespace dev {
+
+static_assert(sizeof(ScD) == sizeof(sc), "scalar layout");
+static_assert(sizeof(PtD) == sizeof(ge), "point layout");
+
+#define AS_SC(p) reinterpret_cast<sc *>(p)
+#define AS_CSC(p) reinterpret_cast<const sc *>(p)
+#define AS_GE(p) reinterpret_cast<ge *>(p)
+#define AS_CGE(p) reinterpret_cast<const ge *>(p)
+
+static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// ===========================================================================
+// point kernels
+// ===========================================================================
+__global__ void k_gens_map(const uint32_t *__restrict__ uni, ge *__restrict__ out, uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t *w = uni + 16 * (size_t)i;
+    fe r1, r2;
+    uint32_t a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) { a[k] = w[k]; b[k] = w[8 + k]; }
+    fe_fromw(r1, a);
+    fe_fromw(r2, b);
+    ge p1, p2, p;
+    ristretto_elligator(p1, r1);
+    ristretto_elligator(p2, r2);
+    ge_add(p, p1, p2);
+    ge_store(out + i, p);
+}
+void launch_gens_map(const uint8_t *uniform, PtD *out, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_gens_map, dim3(nblk(count, 128)), dim3(128), 0, st, (const uint32_t *)uniform, AS_GE(out), count);
+    BPG_HIP(hipGetLastError());
+}
+
+// signed radix-16 digit `w` of a canonical scalar (Scalar::to_radix_16)
+DEVI int radix16_digit(const sc &s, int w) {
+    int carry = 0, d = 0;
+    for (int i = 0; i <= w; i++) {
+        int nib = (s.v[i >> 3] >> (4 * (i & 7))) & 15;
+        int x = nib + carry;
+        carry = (x + 8) >> 4;
+        d = x - (carry << 4);
+    }
+    if (w == 63) d += carry << 4;   // top digit is not recentred
+    return d;
+}
+
+// one wave per commitment: lane w adds the window-w table entries, then an
+// LDS tree reduction (6 levels) instead of a 64-step serial chain.
+__global__ __launch_bounds__(64) void k_pedersen(const sc *__restrict__ v, const sc *__restrict__ vb, uint32_t count,
+                                                 const ge *__restrict__ tB, const ge *__restrict__ tBb,
+                                                 uint32_t *__restrict__ out) {
+    __shared__ ge sh[64];
+    uint32_t idx = blockIdx.x, lane = threadIdx.x;
+    if (idx >= count) return;
+    sc s1, s2, t;
+    sc_load(t, v + idx); sc_reduce(s1, t);
+    sc_load(t, vb + idx); sc_reduce(s2, t);
+    int d1 = radix16_digit(s1, lane), d2 = radix16_digit(s2, lane);
+    ge acc, q;
+    ge_identity(acc);
+    if (d1) { ge_load(q, tB + 8 * lane + (d1 > 0 ? d1 : -d1) - 1); if (d1 < 0) ge_neg(q, q); acc = q; }
+    if (d2) { ge_load(q, tBb + 8 * lane + (d2 > 0 ? d2 : -d2) - 1); if (d2 < 0) ge_neg(q, q); ge_add(acc, acc, q); }
+    ge_store(&sh[lane], acc);
+    for (int s = 32; s >= 1; s >>= 1) {
+        __syncthreads();
+        if (lane < (uint32_t)s) {
+            ge a, b;
+            ge_load(a, &sh[lane]); ge_load(b, &sh[lane + s]);
+            ge_add(a, a, b);
+            ge_store(&sh[lane], a);
+        }
+    }
+    if (lane == 0) {
+        ge r; ge_load(r, &sh[0]);
+        ristretto_encode(out + 8 * (size_t)idx, r);
+    }
+}
+void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tabB, const PtD *tabBb,
+                     uint32_t *out_compressed, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_pedersen, dim3(count), dim3(64), 0, st, AS_CSC(v), AS_CSC(vb), count, AS_CGE(tabB),
+                       AS_CGE(tabBb), out_compressed);
+    BPG_HIP(hipGetLastError());
+}
+
+__global__ void k_compress(const ge *__restrict__ in, uint32_t *__restrict__ out, uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    ge p; ge_load(p, in + i);
+    ristretto_encode(out + 8 * (size_t)i, p);
+}
+void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_compress, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGE(in), out, count);
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_decompress(const uint32_t *__restrict__ in, ge *__restrict__ out, int *ok, uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = in[8 * (size_t)i + k];
+    ge p;
+    bool good = ristretto_decode(p, w);
+    if (!good) { ge_identity(p); atomicAnd(ok, 0); }
+    ge_store(out + i, p);
+}
+void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_decompress, dim3(nblk(count, 64)), dim3(64), 0, st, in, AS_GE(out), ok, count);
+    BPG_HIP(hipGetLastError());
+}
+
+// ===========================================================================
+// Pippenger MSM
+// ===========================================================================
+struct SegTab {
+    const sc *scal[8];
+    const ge *base[8];
+    uint32_t gofs[9];
+    uint32_t row0[8];
+    int n;
+};
+DEVI int seg_of(const SegTab &T, uint32_t g) {
+    int si = 0;
+#pragma unroll
+    for (int k = 1; k < 8; k++) if (k < T.n && g >= T.gofs[k]) si = k;
+    return si;
+}
+
+// signed c-bit windows; key = row * half + (|d| - 1), val = point | sign << 31
+__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t half, uint32_t invalid,
+                             uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    int si = seg_of(T, g);
+    sc k;
+    sc_load(k, T.scal[si] + (g - T.gofs[si]));
+    uint32_t carry = 0, mask = (1u << c) - 1, full = 1u << c;
+    uint32_t row = T.row0[si];
+    for (int w = 0; w < W; w++) {
+        int bit = w * c;
+        int lo = bit >> 5, sh = bit & 31;
+        uint64_t x = k.v[lo];
+        if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
+        uint32_t d = (uint32_t)(x >> sh) & mask;
+        d += carry;
+        uint32_t key = invalid, val = g;
+        if (d > half) {
+            uint32_t mag = full - d;
+            carry = 1;
+            if (mag) { key = (row + w) * half + (mag - 1); val = g | 0x80000000u; }
+        } else {
+            carry = 0;
+            if (d) key = (row + w) * half + (d - 1);
+        }
+        keys[(size_t)w * total + g] = key;
+        vals[(size_t)w * total + g] = val;
+    }
+}
+
+// run starts per chunk (first pass: E given on host; later: read from device)
+__global__ void k_rbk_count(const uint32_t *__restrict__ keys, uint64_t E_host, const uint32_t *E_dev, uint32_t T,
+                            uint32_t invalid, uint32_t nchunks, uint32_t *__restrict__ cnt) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nchunks) return;
+    uint64_t E = E_dev ? *E_dev : E_host;
+    uint64_t s = (uint64_t)j * T, e = s + T;
+    if (e > E) e = E;
+    uint32_t c = 0;
+    uint32_t prev = 0xffffffffu;
+    for (uint64_t i = s; i < e; i++) {
+        uint32_t k = keys[i];
+        if (k != invalid && (i == s || k != prev)) c++;
+        prev = k;
+    }
+    cnt[j] = (s < E) ? c : 0;
+}
+__global__ void k_rbk_total(const uint32_t *cnt, const uint32_t *off, uint32_t nchunks, uint32_t *E_out) {
+    *E_out = off[nchunks - 1] + cnt[nchunks - 1];
+}
+
+DEVI void msm_gather(ge &p, const SegTab &T, uint32_t v) {
+    uint32_t g = v & 0x7fffffffu;
+    int si = seg_of(T, g);
+    ge_load(p, T.base[si] + (g - T.gofs[si]));
+    if (v >> 31) ge_neg(p, p);
+}
+// reduce consecutive equal keys inside each chunk; first pass gathers bases
+__global__ void k_rbk_sum(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                          const ge *__restrict__ pin, SegTab T, uint64_t E_host, const uint32_t *E_dev,
+                          uint32_t chunk, uint32_t invalid, uint32_t nchunks, const uint32_t *__restrict__ off,
+                          uint32_t *__restrict__ kout, ge *__restrict__ pout) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nchunks) return;
+    uint64_t E = E_dev ? *E_dev : E_host;
+    uint64_t s = (uint64_t)j * chunk, e = s + chunk;
+    if (s >= E) return;
+    if (e > E) e = E;
+    uint32_t o = off[j];
+    uint32_t cur = keys[s];
+    if (cur == invalid) return;
+    ge acc, p;
+    if (pin) ge_load(acc, pin + s); else msm_gather(acc, T, vals[s]);
+    for (uint64_t i = s + 1; i < e; i++) {
+        uint32_t k = keys[i];
+        if (k == invalid) break;
+        if (pin) ge_load(p, pin + i); else msm_gather(p, T, vals[i]);
+        if (k == cur) {
+            ge_add(acc, acc, p);
+        } else {
+            kout[o] = cur; ge_store(pout + o, acc); o++;
+            cur = k; acc = p;
+        }
+    }
+    kout[o] = cur;
+    ge_store(pout + o, acc);
+}
+__global__ void k_fill_identity(ge *__restrict__ b, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    ge id; ge_identity(id);
+    ge_store(b + i, id);
+}
+__global__ void k_scatter(const uint32_t *__restrict__ keys, const ge *__restrict__ pts, const uint32_t *E_dev,
+                          uint64_t cap, ge *__restrict__ buckets) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || i >= *E_dev) return;
+    ge p; ge_load(p, pts + i);
+    ge_store(buckets + keys[i], p);
+}
+// sum_{b in seg} (b+1) * S_b = acc + lo * run, with acc weights 1..seglen
+DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {
+    ge_identity(r);
+    if (!k) return;
+    int top = 31 - __clz(k);
+    r = p;
+    for (int b = top - 1; b >= 0; b--) {
+        ge_dbl(r, r);
+        if ((k >> b) & 1) ge_add(r, r, p);
+    }
+}
+__global__ void k_bucket_seg(const ge *__restrict__ buckets, uint32_t rows, uint32_t half, uint32_t seglen,
+                             uint32_t nseg, ge *__restrict__ segacc) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= rows * nseg) return;
+    uint32_t row = t / nseg, s = t % nseg;
+    uint32_t lo = s * seglen;
+    const ge *B = buckets + (size_t)row * half + lo;
+    ge run, acc, p;
+    ge_load(run, B + seglen - 1);
+    acc = run;
+    for (int b = (int)seglen - 2; b >= 0; b--) {
+        ge_load(p, B + b);
+        ge_add(run, run, p);
+        ge_add(acc, acc, run);
+    }
+    if (lo) {
+        ge_mul_small(p, run, lo);
+        ge_add(acc, acc, p);
+    }
+    ge_store(segacc + t, acc);
+}
+__global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segacc, uint32_t nseg,
+                                                    ge *__restrict__ rows_out) {
+    __shared__ ge sh[256];
+    uint32_t row = blockIdx.x, tid = threadIdx.x;
+    const ge *S = segacc + (size_t)row * nseg;
+    ge acc, p;
+    ge_identity(acc);
+    for (uint32_t s = tid; s < nseg; s += 256) { ge_load(p, S + s); ge_add(acc, acc, p); }
+    ge_store(&sh[tid], acc);
+    for (int w = 128; w >= 1; w >>= 1) {
+        __syncthreads();
+        if (tid < (uint32_t)w) {
+            ge a, b;
+            ge_load(a, &sh[tid]); ge_load(b, &sh[tid + w]);
+            ge_add(a, a, b);
+            ge_store(&sh[tid], a);
+        }
+    }
+    if (tid == 0) { ge r; ge_load(r, &sh[0]); ge_store(rows_out + row, r); }
+}
+
+static int msm_window(uint64_t total) {
+    int lg = 0;
+    while ((1ULL << (lg + 1)) <= total) lg++;
+    int c = lg - 3;
+    if (c < 4) c = 4;
+    if (c > 16) c = 16;
+    return c;
+}
+
+MsmEngine::~MsmEngine() {
+    DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &scan_tmp_, &cnt_, &off_, &E_,
+                    &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &segacc_, &rows_dev_};
+    for (DBuf *b : bufs)
+        if (b->p) (void)hipFree(b->p);
+}
+
+void DBuf::grow(size_t need) {
+    if (need <= cap) return;
+    if (p) BPG_HIP(hipFree(p));
+    p = nullptr;
+    size_t n = need + need / 4 + 256;
+    BPG_HIP(hipMalloc(&p, n));
+    cap = n;
+}
+
+void MsmEngine::reserve(const MsmPlan &p) {
+    size_t kb = p.E0 * 4;
+    keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
+    sort_tmp_.grow(p.sort_tmp);
+    scan_tmp_.grow(p.scan_tmp);
+    uint64_t nch = (p.E0 + p.T - 1) / p.T + 1;
+    cnt_.grow(nch * 4); off_.grow(nch * 4);
+    E_.grow(64 * 4);
+    rk_a_.grow(p.capE * 4); rk_b_.grow(p.capE * 4);
+    rp_a_.grow(p.capE * 128); rp_b_.grow(p.capE * 128);
+    buckets_.grow((size_t)p.rows * p.half * 128);
+    segacc_.grow((size_t)p.rows * p.nseg_per_row * 128);
+    rows_dev_.grow((size_t)p.rows * 128);
+}
+
+MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host) {
+    if (nseg < 1 || nseg > 8) throw HipError(hipErrorInvalidValue, "nseg", __FILE__, __LINE__);
+    MsmPlan p{};
+    SegTab T{};
+    uint64_t total = 0;
+    T.n = nseg;
+    for (int i = 0; i < nseg; i++) { T.gofs[i] = (uint32_t)total; total += segs[i].count; }
+    T.gofs[nseg] = (uint32_t)total;
+    p.total = total;
+    p.c = msm_window(total);
+    p.W = (254 + p.c - 1) / p.c;
+    p.nmsm = nmsm;
+    p.rows = nmsm * p.W;
+    p.half = 1 << (p.c - 1);
+    for (int i = 0; i < nseg; i++) {
+        T.scal[i] = AS_CSC(segs[i].scal);
+        T.base[i] = AS_CGE(segs[i].base);
+        T.row0[i] = segs[i].msm * p.W;
+    }
+    p.E0 = (uint64_t)p.W * total;
+    p.T = 32;
+    uint64_t D = (uint64_t)p.rows * p.half;
+    uint32_t invalid = (uint32_t)D;
+    p.key_bits = 1;
+    while ((1ULL << p.key_bits) <= D) p.key_bits++;
+    p.capE = std::min<uint64_t>(p.E0, D + (p.E0 + p.T - 1) / p.T + 1);
+    // passes: enough that T^passes exceeds the largest possible run (total)
+    p.passes = 1;
+    { uint64_t r = p.T; while (r < total + 1) { r *= p.T; p.passes++; } }
+    p.passes += 1;
+    p.seglen = p.half < 16 ? p.half : 16;
+    p.nseg_per_row = p.half / p.seglen;
+    if (total == 0) {
+        for (int r = 0; r < p.rows; r++) {
+            ge id;
+            uint32_t *w = reinterpret_cast<uint32_t *>(&rows_host[r]);
+            memset(w, 0, 128); w[8] = 1; w[16] = 1;
+            (void)id;
+        }
+        return p;
+    }
+    // temp sizes
+    {
+        size_t s = 0;
+        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (uint32_t *)nullptr, (int)p.E0, 0, (int)p.key_bits, st_);
+        p.sort_tmp = s;
+        size_t s2 = 0;
+        uint64_t nch = (p.E0 + p.T - 1) / p.T;
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nch, st_);
+        p.scan_tmp = s2;
+    }
+    reserve(p);
+    uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
+    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
+                       (uint32_t)p.half, invalid, keys, vals);
+    BPG_HIP(hipGetLastError());
+    size_t sbytes = p.sort_tmp;
+    BPG_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, sbytes, keys, keys2, vals, vals2, (int)p.E0, 0,
+                                               (int)p.key_bits, st_));
+    uint32_t *cnt = (uint32_t *)cnt_.p, *off = (uint32_t *)off_.p, *Ed = (uint32_t *)E_.p;
+    const uint32_t *kin = keys2;
+    const ge *pin = nullptr;
+    uint32_t *kout = (uint32_t *)rk_a_.p;
+    ge *pout = AS_GE(rp_a_.p);
+    uint64_t Ebound = p.E0;
+    const uint32_t *Ein = nullptr;
+    for (int pass = 0; pass < p.passes; pass++) {
+        uint32_t nch = (uint32_t)((Ebound + p.T - 1) / p.T);
+        if (nch == 0) nch = 1;
+        hipLaunchKernelGGL(k_rbk_count, dim3(nblk(nch, 256)), dim3(256), 0, st_, kin, Ebound, Ein, p.T, invalid, nch, cnt);
+        size_t tb = p.scan_tmp;
+        BPG_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp_.p, tb, cnt, off, (int)nch, st_));
+        hipLaunchKernelGGL(k_rbk_total, dim3(1), dim3(1), 0, st_, cnt, off, nch, Ed + pass);
+        hipLaunchKernelGGL(k_rbk_sum, dim3(nblk(nch, 64)), dim3(64), 0, st_, kin, (const uint32_t *)vals2, pin, T,
+                           Ebound, Ein, p.T, invalid, nch, off, kout, pout);
+        BPG_HIP(hipGetLastError());
+        // next pass reads this output
+        Ein = Ed + pass;
+        Ebound = std::min<uint64_t>(Ebound, p.capE);
+        kin = kout;
+        pin = pout;
+        kout = (kout == (uint32_t *)rk_a_.p) ? (uint32_t *)rk_b_.p : (uint32_t *)rk_a_.p;
+        pout = (pout == AS_GE(rp_a_.p)) ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
+    }
+    hipLaunchKernelGGL(k_fill_identity, dim3(nblk(D, 256)), dim3(256), 0, st_, AS_GE(buckets_.p), D);
+    hipLaunchKernelGGL(k_scatter, dim3(nblk(Ebound, 256)), dim3(256), 0, st_, kin, pin, Ein, Ebound, AS_GE(buckets_.p));
+    uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
+    hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), (uint32_t)p.rows,
+                       (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, AS_GE(segacc_.p));
+    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, AS_CGE(segacc_.p), (uint32_t)p.nseg_per_row,
+                       AS_GE(rows_dev_.p));
+    BPG_HIP(hipGetLastError());
+    BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * 128, hipMemcpyDeviceToHost, st_));
+    return p;
+}
+
+// ===========================================================================
+// scalar-vector kernels (Montgomery domain noted per kernel)
+// ===========================================================================
+DEVI void mm(sc &r, const sc &a, const sc &b) { sc_montmul(r, a, b); }
+DEVI sc sc_one_raw() { sc o; sc_zero(o); o.v[0] = 1; return o; }
+
+// out[i] = mont(base^(start+i)); base2[b] = mont(base^(2^b))
+__global__ void k_pow_table(const sc *__restrict__ base2, uint64_t start, uint32_t count, sc *__restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint64_t e = start + i;
+    // mont(1) = R mod l
+    sc acc;
+    acc.v[0] = 0x8d98951du; acc.v[1] = 0xd6ec3174u; acc.v[2] = 0x737dcf70u; acc.v[3] = 0xc6ef5bf4u;
+    acc.v[4] = 0xfffffffeu; acc.v[5] = 0xffffffffu; acc.v[6] = 0xffffffffu; acc.v[7] = 0x0fffffffu;
+    for (int b = 0; b < 40 && e; b++, e >>= 1) {
+        if (e & 1) { sc t; sc_load(t, base2 + b); mm(acc, acc, t); }
+    }
+    sc_store(out + i, acc);
+}
+void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_pow_table, dim3(nblk(count, 128)), dim3(128), 0, st, AS_CSC(base2), start, count, AS_SC(out));
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_pow_expand(const sc *__restrict__ lo, const sc *__restrict__ hi, uint32_t count, sc *__restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    sc a, b, r;
+    sc_load(a, lo + (i & 1023)); sc_load(b, hi + (i >> 10));
+    mm(r, a, b);
+    sc_store(out + i, r);
+}
+void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD *out, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_pow_expand, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(lo), AS_CSC(hi), count, AS_SC(out));
+    BPG_HIP(hipGetLastError());
+}
+
+// flatten: z tables are Montgomery; result normal form
+DEVI void flat_term(sc &acc, uint32_t q, const sc &coeff, const sc *zlo, const sc *zhi) {
+    uint32_t e = q + 1;
+    sc a, b, zm, t;
+    sc_load(a, zlo + (e & 1023)); sc_load(b, zhi + (e >> 10));
+    mm(zm, a, b);
+    mm(t, coeff, zm);
+    sc_add(acc, acc, t);
+}
+__global__ void k_flatten_short(CscDev c, const sc *__restrict__ zlo, const sc *__restrict__ zhi, sc *__restrict__ out) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= c.nshort) return;
+    uint32_t col = c.short_cols[t];
+    sc acc; sc_zero(acc);
+    for (uint32_t k = c.col_ptr[col]; k < c.col_ptr[col + 1]; k++) {
+        sc co; sc_load(co, AS_CSC(c.coeff) + k);
+        flat_term(acc, c.row[k], co, zlo, zhi);
+    }
+    if (col >= c.neg_from) sc_neg(acc, acc);
+    sc_store(out + col, acc);
+}
+__global__ __launch_bounds__(64) void k_flatten_long(CscDev c, const sc *__restrict__ zlo, const sc *__restrict__ zhi,
+                                                     sc *__restrict__ out) {
+    __shared__ sc sh[64];
+    uint32_t t = blockIdx.x, lane = threadIdx.x;
+    if (t >= c.nlong) return;
+    uint32_t col = c.long_cols[t];
+    sc acc; sc_zero(acc);
+    for (uint32_t k = c.col_ptr[col] + lane; k < c.col_ptr[col + 1]; k += 64) {
+        sc co; sc_load(co, AS_CSC(c.coeff) + k);
+        flat_term(acc, c.row[k], co, zlo, zhi);
+    }
+    sc_store(&sh[lane], acc);
+    for (int s = 32; s >= 1; s >>= 1) {
+        __syncthreads();
+        if (lane < (uint32_t)s) { sc a, b; sc_load(a, &sh[lane]); sc_load(b, &sh[lane + s]); sc_add(a, a, b); sc_store(&sh[lane], a); }
+    }
+    if (lane == 0) {
+        sc r; sc_load(r, &sh[0]);
+        if (col >= c.neg_from) sc_neg(r, r);
+        sc_store(out + col, r);
+    }
+}
+void launch_flatten(const CscDev &csc, const ScD *zlo, const ScD *zhi, ScD *out, hipStream_t st) {
+    if (csc.nshort)
+        hipLaunchKernelGGL(k_flatten_short, dim3(nblk(csc.nshort, 128)), dim3(128), 0, st, csc, AS_CSC(zlo), AS_CSC(zhi), AS_SC(out));
+    if (csc.nlong)
+        hipLaunchKernelGGL(k_flatten_long, dim3(csc.nlong), dim3(64), 0, st, csc, AS_CSC(zlo), AS_CSC(zhi), AS_SC(out));
+    BPG_HIP(hipGetLastError());
+}
+
+__global__ void k_lr_build(const sc *__restrict__ aL, const sc *__restrict__ aR, const sc *__restrict__ sR,
+                           const sc *__restrict__ wL, const sc *__restrict__ wR, const sc *__restrict__ wO,
+                           const sc *__restrict__ ypm, const sc *__restrict__ yipm, uint32_t n, sc *__restrict__ l1,
+                           sc *__restrict__ r0, sc *__restrict__ r1, sc *__restrict__ r3) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    sc a, b, y, t, u;
+    sc_load(y, ypm + i);
+    sc_load(t, yipm + i); sc_load(b, wR + i); mm(u, t, b); sc_load(a, aL + i); sc_add(u, a, u); sc_store(l1 + i, u);
+    sc one = sc_one_raw(), yn;
+    mm(yn, y, one);
+    sc_load(a, wO + i); sc_sub(u, a, yn); sc_store(r0 + i, u);
+    sc_load(a, aR + i); mm(u, y, a); sc_load(b, wL + i); sc_add(u, u, b); sc_store(r1 + i, u);
+    sc_load(a, sR + i); mm(u, y, a); sc_store(r3 + i, u);
+}
+void launch_lr_build(const ScD *aL, const ScD *aR, const ScD *sR, const ScD *wL, const ScD *wR, const ScD *wO,
+                     const ScD *yp, const ScD *yip, uint32_t n, ScD *l1, ScD *r0, ScD *r1, ScD *r3, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_lr_build, dim3(nblk(n, 128)), dim3(128), 0, st, AS_CSC(aL), AS_CSC(aR), AS_CSC(sR), AS_CSC(wL),
+                       AS_CSC(wR), AS_CSC(wO), AS_CSC(yp), AS_CSC(yip), n, AS_SC(l1), AS_SC(r0), AS_SC(r1), AS_SC(r3));
+    BPG_HIP(hipGetLastError());
+}
+
+// block reduction of K scalars per thread into partial[block*K + k]
+template <int K>
+DEVI void block_reduce_store(sc (&v)[K], sc *__restrict__ partial) {
+    __shared__ sc sh[256];
+    uint32_t tid = threadIdx.x;
+    for (int k = 0; k < K; k++) {
+        sc_store(&sh[tid], v[k]);
+        for (int s = 128; s >= 1; s >>= 1) {
+            __syncthreads();
+            if (tid < (uint32_t)s) { sc a, b; sc_load(a, &sh[tid]); sc_load(b, &sh[tid + s]); sc_add(a, a, b); sc_store(&sh[tid], a); }
+        }
+        __syncthreads();
+        if (tid == 0) { sc r; sc_load(r, &sh[0]); sc_store(partial + blockIdx.x * K + k, r); }
+        __syncthreads();
+    }
+}
+#define RED_BLOCKS 1024
+// Montgomery-scaled sums (sum a*b/R); the final reduce multiplies by R^2/R
+__global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const sc *__restrict__ l2,
+                                               const sc *__restrict__ l3, const sc *__restrict__ r0,
+                                               const sc *__restrict__ r1, const sc *__restrict__ r3, uint32_t n,
+                                               sc *__restrict__ partial) {
+    sc acc[6];
+    for (int k = 0; k < 6; k++) sc_zero(acc[k]);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        sc a1, a2, a3, b0, b1, b3, t;
+        sc_load(a1, l1 + i); sc_load(a2, l2 + i); sc_load(a3, l3 + i);
+        sc_load(b0, r0 + i); sc_load(b1, r1 + i); sc_load(b3, r3 + i);
+        mm(t, a1, b0); sc_add(acc[0], acc[0], t);                                   // t1 = l1.r0
+        mm(t, a1, b1); sc_add(acc[1], acc[1], t); mm(t, a2, b0); sc_add(acc[1], acc[1], t);  // t2
+        mm(t, a2, b1); sc_add(acc[2], acc[2], t); mm(t, a3, b0); sc_add(acc[2], acc[2], t);  // t3
+        mm(t, a1, b3); sc_add(acc[3], acc[3], t); mm(t, a3, b1); sc_add(acc[3], acc[3], t);  // t4
+        mm(t, a2, b3); sc_add(acc[4], acc[4], t);                                   // t5
+        mm(t, a3, b3); sc_add(acc[5], acc[5], t);                                   // t6
+    }
+    block_reduce_store<6>(acc, partial);
+}
+// out[k] = R * sum_b partial[b*K + k]   (one block per k)
+__global__ __launch_bounds__(256) void k_reduce_cols(const sc *__restrict__ partial, uint32_t nb, uint32_t K,
+                                                     sc *__restrict__ out, uint32_t out_stride) {
+    __shared__ sc sh[256];
+    uint32_t k = blockIdx.x, tid = threadIdx.x;
+    sc acc; sc_zero(acc);
+    for (uint32_t b = tid; b < nb; b += 256) { sc t; sc_load(t, partial + (size_t)b * K + k); sc_add(acc, acc, t); }
+    sc_store(&sh[tid], acc);
+    for (int s = 128; s >= 1; s >>= 1) {
+        __syncthreads();
+        if (tid < (uint32_t)s) { sc a, b; sc_load(a, &sh[tid]); sc_load(b, &sh[tid + s]); sc_add(a, a, b); sc_store(&sh[tid], a); }
+    }
+    if (tid == 0) {
+        sc r, r2;
+        sc_load(r, &sh[0]);
+        for (int i = 0; i < 8; i++) r2.v[i] = SC_R2[i];
+        mm(r, r, r2);
+        sc_store(out + (size_t)k * out_stride, r);
+    }
+}
+void launch_tpoly(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, const ScD *r1, const ScD *r3,
+                  uint32_t n, ScD *partial, ScD *out6, hipStream_t st) {
+    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(n, 256)));
+    hipLaunchKernelGGL(k_tpoly, dim3(nb), dim3(256), 0, st, AS_CSC(l1), AS_CSC(l2), AS_CSC(l3), AS_CSC(r0),
+                       AS_CSC(r1), AS_CSC(r3), n, AS_SC(partial));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(6), dim3(256), 0, st, AS_CSC(partial), nb, 6u, AS_SC(out6), 1u);
+    BPG_HIP(hipGetLastError());
+}
+__global__ __launch_bounds__(256) void k_dot(const sc *__restrict__ a, const sc *__restrict__ b, uint32_t n,
+                                             sc *__restrict__ partial) {
+    sc acc[1];
+    sc_zero(acc[0]);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        sc x, y, t;
+        sc_load(x, a + i); sc_load(y, b + i);
+        mm(t, x, y); sc_add(acc[0], acc[0], t);
+    }
+    block_reduce_store<1>(acc, partial);
+}
+void launch_dot(const ScD *a, const ScD *b, uint32_t n, ScD *partial, ScD *out, hipStream_t st) {
+    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(n, 256)));
+    hipLaunchKernelGGL(k_dot, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), n, AS_SC(partial));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(256), 0, st, AS_CSC(partial), nb, 1u, AS_SC(out), 1u);
+    BPG_HIP(hipGetLastError());
+}
+
+// x given in Montgomery form (x*R); l2 = a_O, l3 = s_L
+__global__ void k_lr_eval(const sc *__restrict__ l1, const sc *__restrict__ l2, const sc *__restrict__ l3,
+                          const sc *__restrict__ r0, const sc *__restrict__ r1, const sc *__restrict__ r3,
+                          const sc *__restrict__ ypm, uint32_t n, uint32_t N, sc xm, sc x2m, sc *__restrict__ a,
+                          sc *__restrict__ b) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    sc ra, rb;
+    if (i < n) {
+        sc p, q, t;
+        sc_load(p, l3 + i); mm(t, p, xm); sc_load(q, l2 + i); sc_add(t, t, q); mm(t, t, xm);
+        sc_load(q, l1 + i); sc_add(t, t, q); mm(ra, t, xm);
+        sc_load(p, r3 + i); mm(t, p, x2m); sc_load(q, r1 + i); sc_add(t, t, q); mm(t, t, xm);
+        sc_load(q, r0 + i); sc_add(rb, t, q);
+    } else {
+        sc y, one = sc_one_raw();
+        sc_load(y, ypm + i); mm(y, y, one);
+        sc_zero(ra);
+        sc_neg(rb, y);
+    }
+    sc_store(a + i, ra);
+    sc_store(b + i, rb);
+}
+void launch_lr_eval(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, const ScD *r1, const ScD *r3,
+                    const ScD *yp, uint32_t n, uint32_t N, ScD xm, ScD x2m, ScD *a, ScD *b, hipStream_t st) {
+    hipLaunchKernelGGL(k_lr_eval, dim3(nblk(N, 128)), dim3(128), 0, st, AS_CSC(l1), AS_CSC(l2), AS_CSC(l3), AS_CSC(r0),
+                       AS_CSC(r1), AS_CSC(r3), AS_CSC(yp), n, N, *reinterpret_cast<sc *>(&xm),
+                       *reinterpret_cast<sc *>(&x2m), AS_SC(a), AS_SC(b));
+    BPG_HIP(hipGetLastError());
+}
+
+// ===========================================================================
+// IPP
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                  const sc *__restrict__ yipm, IppRoundArgs A, sc *__restrict__ out,
+                                                  sc *__restrict__ partial) {
+    sc acc[2];
+    sc_zero(acc[0]); sc_zero(acc[1]);
+    const uint32_t h = A.h;
+    const sc lamG1 = *reinterpret_cast<const sc *>(&A.lamG1), lamGu = *reinterpret_cast<const sc *>(&A.lamGu);
+    const sc muH1 = *reinterpret_cast<const sc *>(&A.muH1), muHu = *reinterpret_cast<const sc *>(&A.muHu);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < h; i += gridDim.x * blockDim.x) {
+        sc aL, aR, bL, bR, t, y;
+        sc_load(aL, a + i); sc_load(aR, a + h + i); sc_load(bL, b + i); sc_load(bR, b + h + i);
+        mm(t, aL, bR); sc_add(acc[0], acc[0], t);
+        mm(t, aR, bL); sc_add(acc[1], acc[1], t);
+        bool lo_real = i < A.n, hi_real = (h + i) < A.n;
+        // L: aL * lam*Gf[h+i] (base Ghat_R), bR * mu*Gf[i]*y^-i (base Hhat_L)
+        mm(t, aL, hi_real ? lamG1 : lamGu); sc_store(out + i, t);
+        sc_load(y, yipm + i); mm(t, bR, y); mm(t, t, lo_real ? muH1 : muHu); sc_store(out + h + i, t);
+        // R: aR * lam*Gf[i] (base Ghat_L), bL * mu*Gf[h+i]*y^-(h+i) (base Hhat_R)
+        mm(t, aR, lo_real ? lamG1 : lamGu); sc_store(out + 2 * h + i, t);
+        sc_load(y, yipm + h + i); mm(t, bL, y); mm(t, t, hi_real ? muH1 : muHu); sc_store(out + 3 * h + i, t);
+    }
+    block_reduce_store<2>(acc, partial);
+}
+void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
+                     ScD *partial, hipStream_t st) {
+    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
+    hipLaunchKernelGGL(k_ipp_prep, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args,
+                       AS_SC(msm_scal), AS_SC(partial));
+    // c_L -> msm_scal[4h], c_R -> msm_scal[4h+1]
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
+                       AS_SC(msm_scal + 4 * (size_t)args.h), 1u);
+    BPG_HIP(hipGetLastError());
+}
+// u, uinv in Montgomery form
+__global__ void k_ipp_fold_scalars(sc *__restrict__ a, sc *__restrict__ b, uint32_t h, sc um, sc uim) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= h) return;
+    sc x, y, t1, t2;
+    sc_load(x, a + i); sc_load(y, a + h + i); mm(t1, x, um); mm(t2, y, uim); sc_add(t1, t1, t2); sc_store(a + i, t1);
+    sc_load(x, b + i); sc_load(y, b + h + i); mm(t1, x, uim); mm(t2, y, um); sc_add(t1, t1, t2); sc_store(b + i, t1);
+}
+void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st) {
+    hipLaunchKernelGGL(k_ipp_fold_scalars, dim3(nblk(h, 256)), dim3(256), 0, st, AS_SC(a), AS_SC(b), h,
+                       *reinterpret_cast<sc *>(&u), *reinterpret_cast<sc *>(&uinv));
+    BPG_HIP(hipGetLastError());
+}
+// NAF double-and-add of a (per-lane selected) scalar, then + P_L
+DEVI void naf_mul_add(ge &out, const ge &PL, const ge &PR, const sc &k0) {
+    // NAF digits LSB-first into pos/neg bitmasks (<= 254 digits for k < 2^253)
+    uint32_t pos[9], neg[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) { pos[i] = 0; neg[i] = 0; }
+    uint32_t k[9];
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = k0.v[i];
+    k[8] = 0;
+    int top = -1;
+    for (int bit = 0; bit < 260; bit++) {
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < 9; i++) any = any || k[i];
+        if (!any) break;
+        if (k[0] & 1) {
+            uint32_t r = k[0] & 3;
+            if (r == 1) {
+                pos[bit >> 5] |= 1u << (bit & 31);
+                k[0] &= ~1u;
+            } else {
+                neg[bit >> 5] |= 1u << (bit & 31);
+                // k += 1
+                uint64_t c = 1;
+#pragma unroll
+                for (int i = 0; i < 9; i++) { c += k[i]; k[i] = (uint32_t)c; c >>= 32; }
+            }
+            top = bit;
+        }
+        // k >>= 1
+#pragma unroll
+        for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
+        k[8] >>= 1;
+    }
+    ge acc;
+    if (top < 0) {
+        acc = PL;
+    } else {
+        ge nPR;
+        ge_neg(nPR, PR);
+        acc = ((pos[top >> 5] >> (top & 31)) & 1) ? PR : nPR;
+        for (int bit = top - 1; bit >= 0; bit--) {
+            ge_dbl(acc, acc);
+            if ((pos[bit >> 5] >> (bit & 31)) & 1) ge_add(acc, acc, PR);
+            else if ((neg[bit >> 5] >> (bit & 31)) & 1) ge_add(acc, acc, nPR);
+        }
+        ge_add(acc, acc, PL);
+    }
+    out = acc;
+}
+__global__ void k_ipp_fold_points(const ge *__restrict__ Gin, const ge *__restrict__ Hin, uint32_t h, uint32_t n,
+                                  sc rGa, sc rGb, sc rHa, sc rHb, ge *__restrict__ Gout, ge *__restrict__ Hout) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * h) return;
+    bool isH = t >= h;
+    uint32_t i = isH ? t - h : t;
+    bool special = (i < n) && (h + i >= n);
+    const ge *P = isH ? Hin : Gin;
+    ge PL, PR, r;
+    ge_load(PL, P + i);
+    ge_load(PR, P + h + i);
+    const sc &rho = isH ? (special ? rHb : rHa) : (special ? rGb : rGa);
+    naf_mul_add(r, PL, PR, rho);
+    ge_store((isH ? Hout : Gout) + i, r);
+}
+void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
+                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, hipStream_t st) {
+    hipLaunchKernelGGL(k_ipp_fold_points, dim3(nblk(2 * (uint64_t)h, 64)), dim3(64), 0, st, AS_CGE(Gin), AS_CGE(Hin),
+                       h, n, *reinterpret_cast<sc *>(&rhoG_a), *reinterpret_cast<sc *>(&rhoG_b),
+                       *reinterpret_cast<sc *>(&rhoH_a), *reinterpret_cast<sc *>(&rhoH_b), AS_GE(Gout), AS_GE(Hout));
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_fill_scalars(sc *dst, sc val, uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) sc_store(dst + i, val);
+}
+void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_fill_scalars, dim3(nblk(count, 256)), dim3(256), 0, st, AS_SC(dst), *reinterpret_cast<sc *>(&val), count);
+    BPG_HIP(hipGetLastError());
+}
+
+// Verifier::verify g/h scalars (bulletproofs r1cs/verifier.rs, IPP
+// verification_scalars): s_i = allinv * prod_{bit j of i} u_{lgn-1-j}^2.
+// w = flatten output [wL | wR | wO | ...]; u2m = Montgomery(u_k^2);
+// xm, am, bm, um Montgomery forms of x, ipp.a, ipp.b, r1cs u.
+__global__ void k_verify_gh(const sc *__restrict__ w, const sc *__restrict__ yipm, const sc *__restrict__ u2m,
+                            sc allinv, uint32_t n, uint32_t N, uint32_t lgn, sc xm, sc am, sc bm, sc um,
+                            sc *__restrict__ out, sc *__restrict__ ynwR) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    sc si = allinv, sv = allinv, t;
+    for (uint32_t j = 0; j < lgn; j++) {
+        sc u; sc_load(u, u2m + (lgn - 1 - j));
+        if ((i >> j) & 1) mm(si, si, u);
+        else mm(sv, sv, u);          // bits of N-1-i are the complement of i's
+    }
+    sc yi; sc_load(yi, yipm + i);
+    sc wL, wR, wO;
+    if (i < n) { sc_load(wL, w + i); sc_load(wR, w + n + i); sc_load(wO, w + 2 * n + i); }
+    else { sc_zero(wL); sc_zero(wR); sc_zero(wO); }
+    sc yn; mm(yn, wR, yi);
+    if (i < n) sc_store(ynwR + i, yn);
+    sc g, a;
+    mm(g, yn, xm); mm(a, si, am); sc_sub(g, g, a);
+    if (i >= n) mm(g, g, um);
+    sc h;
+    mm(h, wL, xm); sc_add(h, h, wO); mm(a, sv, bm); sc_sub(h, h, a);
+    mm(h, h, yi);
+    sc one = sc_one_raw();
+    sc_sub(h, h, one);
+    if (i >= n) mm(h, h, um);
+    sc_store(out + i, g);
+    sc_store(out + N + i, h);
+    (void)t;
+}
+void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
+                      ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st) {
+    hipLaunchKernelGGL(k_verify_gh, dim3(nblk(N, 128)), dim3(128), 0, st, AS_CSC(w), AS_CSC(yipm), AS_CSC(u2m),
+                       *reinterpret_cast<sc *>(&allinv), n, N, lgn, *reinterpret_cast<sc *>(&xm),
+                       *reinterpret_cast<sc *>(&am), *reinterpret_cast<sc *>(&bm), *reinterpret_cast<sc *>(&um),
+                       AS_SC(out), AS_SC(ynwR));
+    BPG_HIP(hipGetLastError());
+}
+
+}  // namespace dev
+}  // namespace bpg

@@ -1,0 +1,681 @@
+// r1cs_gpu.cpp — see r1cs_gpu.h.
+// Protocol steps follow bulletproofs@2.1.0 src/r1cs/prover.rs `prove` and
+// src/r1cs/verifier.rs `verify` (one-phase circuits: no deferred
+// constraints), src/inner_product_proof.rs `create` / `verification_scalars`,
+// and src/r1cs/proof.rs `to_bytes` / `from_bytes`.
+#include "r1cs_gpu.h"
+
+#include <algorithm>
+#include <chrono>
+#include <map>
+#include <stdexcept>
+
+namespace bpg {
+using namespace dev;
+
+static inline ScD to_dev(const Scalar &s) { ScD d; memcpy(d.v, s.v, 32); return d; }
+static inline Scalar from_dev(const ScD &d) { Scalar s; memcpy(s.v, d.v, 32); return s; }
+static const Scalar R_MOD_L = {{0xd6ec31748d98951dULL, 0xc6ef5bf4737dcf70ULL, 0xfffffffffffffffeULL, 0x0fffffffffffffffULL}};
+static inline ScD mont(const Scalar &s) { return to_dev(s * R_MOD_L); }
+static uint32_t next_pow2(uint32_t n) { uint32_t p = 1; while (p < n) p <<= 1; return p; }
+static uint32_t lg2u(uint32_t n) { uint32_t k = 0; while ((1u << k) < n) k++; return k; }
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------ context
+static std::mutex g_ctx_mu;
+DeviceContext &DeviceContext::get(int device) {
+    static std::map<int, std::unique_ptr<DeviceContext>> ctxs;
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    auto &p = ctxs[device];
+    if (!p) {
+        p.reset(new DeviceContext());
+        p->device = device;
+        BPG_HIP(hipSetDevice(device));
+        // fixed-base tables for B and B_blinding: T[w][j] = (j+1) 16^w P
+        std::vector<PtD> tab(2 * 512);
+        for (int which = 0; which < 2; which++) {
+            Point base = which ? basepoint_B_blinding() : basepoint_B();
+            for (int w = 0; w < 64; w++) {
+                Point acc = base;
+                for (int j = 0; j < 8; j++) {
+                    pt_to_dev(tab[which * 512 + 8 * w + j].v, acc);
+                    Point t; pt_add(t, acc, base); acc = t;
+                }
+                for (int k = 0; k < 4; k++) pt_dbl(base, base);
+            }
+        }
+        BPG_HIP(hipMalloc(&p->tabB, 1024 * sizeof(PtD)));
+        p->tabBb = p->tabB + 512;
+        BPG_HIP(hipMemcpy(p->tabB, tab.data(), 1024 * sizeof(PtD), hipMemcpyHostToDevice));
+        PtD bb; pt_to_dev(bb.v, basepoint_B_blinding());
+        BPG_HIP(hipMalloc(&p->Bb, sizeof(PtD)));
+        BPG_HIP(hipMemcpy(p->Bb, &bb, sizeof(PtD), hipMemcpyHostToDevice));
+    }
+    return *p;
+}
+
+// BulletproofGens::new(N, 1): chains SHAKE256("GeneratorsChain" || tag || u32le(0))
+// squeezed 64 bytes per point on the host (the XOF is one serial chain),
+// Elligator x2 + add on the device.
+void DeviceContext::ensure_gens(uint32_t N) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (N <= gens_cap) return;
+    uint32_t cap = std::max<uint32_t>(N, 64);
+    BPG_HIP(hipSetDevice(device));
+    PtD *nG = nullptr, *nH = nullptr;
+    BPG_HIP(hipMalloc(&nG, (size_t)cap * sizeof(PtD)));
+    BPG_HIP(hipMalloc(&nH, (size_t)cap * sizeof(PtD)));
+    std::vector<uint8_t> uni((size_t)cap * 64);
+    uint8_t *duni = nullptr;
+    BPG_HIP(hipMalloc(&duni, uni.size()));
+    for (int which = 0; which < 2; which++) {
+        uint8_t label[20];
+        memcpy(label, "GeneratorsChain", 15);
+        label[15] = which ? 'H' : 'G';
+        label[16] = label[17] = label[18] = label[19] = 0;
+        Shake256 xof;
+        xof.init_absorb(label, 20);
+        xof.squeeze(uni.data(), uni.size());
+        BPG_HIP(hipMemcpy(duni, uni.data(), uni.size(), hipMemcpyHostToDevice));
+        launch_gens_map(duni, which ? nH : nG, cap, 0);
+    }
+    BPG_HIP(hipDeviceSynchronize());
+    (void)hipFree(duni);
+    if (G) (void)hipFree(G);
+    if (H) (void)hipFree(H);
+    G = nG; H = nH; gens_cap = cap;
+}
+
+// ---------------------------------------------------------------- workspace
+struct Workspace {
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::unique_ptr<MsmEngine> msm;
+    DBuf sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
+        ynwR, pts, okflag;
+    PtD *rows_host = nullptr;        // pinned, 8 x 64 rows
+    uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
+    size_t s_host_cap = 0;
+    ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
+    ~Workspace() {
+        if (rows_host) (void)hipHostFree(rows_host);
+        if (s_host) (void)hipHostFree(s_host);
+        if (small_host) (void)hipHostFree(small_host);
+        DBuf *bufs[] = {&sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
+                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag};
+        for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
+        msm.reset();
+        if (st) (void)hipStreamDestroy(st);
+    }
+    void stage(size_t bytes) {
+        if (bytes <= s_host_cap) return;
+        if (s_host) BPG_HIP(hipHostFree(s_host));
+        s_host_cap = bytes + bytes / 4 + 4096;
+        BPG_HIP(hipHostMalloc((void **)&s_host, s_host_cap, hipHostMallocDefault));
+    }
+};
+
+Workspace &thread_workspace(int device) {
+    static thread_local std::map<int, std::unique_ptr<Workspace>> wss;
+    auto &p = wss[device];
+    if (!p) {
+        BPG_HIP(hipSetDevice(device));
+        p.reset(new Workspace());
+        p->device = device;
+        BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+        p->msm.reset(new MsmEngine(p->st));
+        BPG_HIP(hipHostMalloc((void **)&p->rows_host, 8 * 64 * sizeof(PtD), hipHostMallocDefault));
+        BPG_HIP(hipHostMalloc((void **)&p->small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
+    }
+    BPG_HIP(hipSetDevice(device));
+    return *p;
+}
+
+ProveTimings &last_timings() { static thread_local ProveTimings t; return t; }
+
+template <class T>
+static T *as(DBuf &b) { return reinterpret_cast<T *>(b.p); }
+
+// ------------------------------------------------------------------ prepare
+PreparedCS::~PreparedCS() {
+    DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols};
+    for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
+}
+
+std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
+    std::unique_ptr<PreparedCS> P(new PreparedCS());
+    BPG_HIP(hipSetDevice(device));
+    P->device = device;
+    P->n = cs->n; P->m = cs->m; P->q = cs->q;
+    P->N = next_pow2(cs->n);
+    P->lgN = lg2u(P->N);
+    P->prover = cs->a_L != nullptr;
+    const uint32_t n = cs->n, m = cs->m;
+    if (n >= (1u << 28) || m >= (1u << 28)) throw std::runtime_error("circuit too large");
+    // constraint matrix, transposed to columns [L | R | O | V | One]
+    const uint32_t ncol = 3 * n + m + 1;
+    P->ncol = ncol;
+    std::vector<uint32_t> cnt(ncol + 1, 0);
+    const uint32_t nnz = cs->row_ptr[cs->q];
+    auto colof = [&](uint32_t var) -> uint32_t {
+        uint32_t kind = BPG_VAR_KIND(var), idx = BPG_VAR_INDEX(var);
+        switch (kind) {
+            case BPG_VAR_ONE: return 3 * n + m;
+            case BPG_VAR_L: if (idx >= n) throw std::runtime_error("bad variable"); return idx;
+            case BPG_VAR_R: if (idx >= n) throw std::runtime_error("bad variable"); return n + idx;
+            case BPG_VAR_O: if (idx >= n) throw std::runtime_error("bad variable"); return 2 * n + idx;
+            case BPG_VAR_V: if (idx >= m) throw std::runtime_error("bad variable"); return 3 * n + idx;
+        }
+        throw std::runtime_error("bad variable kind");
+    };
+    for (uint32_t k = 0; k < nnz; k++) cnt[colof(cs->term_var[k]) + 1]++;
+    for (uint32_t c = 0; c < ncol; c++) cnt[c + 1] += cnt[c];
+    std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1), rows(nnz ? nnz : 1);
+    std::vector<ScD> coef(nnz ? nnz : 1);
+    for (uint32_t q = 0; q < cs->q; q++)
+        for (uint32_t k = cs->row_ptr[q]; k < cs->row_ptr[q + 1]; k++) {
+            uint32_t c = colof(cs->term_var[k]);
+            uint32_t at = pos[c]++;
+            rows[at] = q;
+            coef[at] = to_dev(Scalar::reduce(cs->term_coeff + 32 * (size_t)k));
+        }
+    std::vector<uint32_t> sc_, lc_;
+    for (uint32_t c = 0; c < ncol; c++) ((cnt[c + 1] - cnt[c]) > 16 ? lc_ : sc_).push_back(c);
+    P->nshort = (uint32_t)sc_.size(); P->nlong = (uint32_t)lc_.size();
+    auto up = [&](DBuf &d, const void *src, size_t bytes) {
+        d.grow(bytes ? bytes : 4);
+        if (bytes) BPG_HIP(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
+    };
+    up(P->col_ptr, cnt.data(), cnt.size() * 4);
+    up(P->col_row, rows.data(), rows.size() * 4);
+    up(P->col_coeff, coef.data(), coef.size() * sizeof(ScD));
+    up(P->short_cols, sc_.data(), sc_.size() * 4);
+    up(P->long_cols, lc_.data(), lc_.size() * 4);
+    if (P->prover) {
+        std::vector<ScD> tmp(n ? n : 1);
+        const uint8_t *src[3] = {cs->a_L, cs->a_R, cs->a_O};
+        DBuf *dst[3] = {&P->aL, &P->aR, &P->aO};
+        for (int k = 0; k < 3; k++) {
+            for (uint32_t i = 0; i < n; i++) tmp[i] = to_dev(Scalar::reduce(src[k] + 32 * (size_t)i));
+            up(*dst[k], tmp.data(), (size_t)n * sizeof(ScD));
+        }
+        P->v.resize(m); P->vb.resize(m);
+        std::vector<ScD> vbd(m ? m : 1);
+        for (uint32_t i = 0; i < m; i++) {
+            P->v[i] = Scalar::from_bits(cs->v + 32 * (size_t)i);
+            // keep raw bytes of v (Scalar::from_bits may differ only in bit 255)
+            memcpy(P->v[i].v, cs->v + 32 * (size_t)i, 32);
+            P->vb[i] = Scalar::reduce(cs->v_blinding + 32 * (size_t)i);
+            memcpy(P->vb[i].v, cs->v_blinding + 32 * (size_t)i, 32);
+            vbd[i] = to_dev(P->vb[i].reduced());
+        }
+        up(P->vb_dev, vbd.data(), (size_t)m * sizeof(ScD));
+        P->V.resize((size_t)m * 32);
+        if (m) gpu_pedersen(device, P->v, P->vb, P->V.data());
+    }
+    return P;
+}
+
+void gpu_pedersen(int device, const std::vector<Scalar> &v, const std::vector<Scalar> &vb, uint8_t *out) {
+    DeviceContext &ctx = DeviceContext::get(device);
+    Workspace &ws = thread_workspace(device);
+    const uint32_t m = (uint32_t)v.size();
+    if (!m) return;
+    std::vector<ScD> h(2 * (size_t)m);
+    for (uint32_t i = 0; i < m; i++) { memcpy(h[i].v, v[i].v, 32); memcpy(h[m + i].v, vb[i].v, 32); }
+    ws.small.grow(2 * (size_t)m * sizeof(ScD) + (size_t)m * 32);
+    ScD *d = as<ScD>(ws.small);
+    BPG_HIP(hipMemcpyAsync(d, h.data(), 2 * (size_t)m * sizeof(ScD), hipMemcpyHostToDevice, ws.st));
+    uint32_t *outd = reinterpret_cast<uint32_t *>(d + 2 * (size_t)m);
+    launch_pedersen(d, d + m, m, ctx.tabB, ctx.tabBb, outd, ws.st);
+    BPG_HIP(hipMemcpyAsync(out, outd, (size_t)m * 32, hipMemcpyDeviceToHost, ws.st));
+    BPG_HIP(hipStreamSynchronize(ws.st));
+}
+
+// -------------------------------------------------------------- MSM helpers
+static void combine_rows(Point &out, const PtD *rows, int W, int c) {
+    Point acc;
+    pt_from_dev(acc, rows[W - 1].v);
+    for (int w = W - 2; w >= 0; w--) {
+        for (int k = 0; k < c; k++) pt_dbl(acc, acc);
+        Point r; pt_from_dev(r, rows[w].v);
+        Point t; pt_add(t, acc, r); acc = t;
+    }
+    out = acc;
+}
+
+int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t n, uint8_t out[32]) {
+    DeviceContext::get(device);
+    Workspace &ws = thread_workspace(device);
+    ws.small.grow((size_t)n * sizeof(ScD) + 64);
+    ws.pts.grow((size_t)n * sizeof(PtD) + 64);
+    ws.okflag.grow(64);
+    std::vector<ScD> s(n ? n : 1);
+    for (uint32_t i = 0; i < n; i++) s[i] = to_dev(Scalar::reduce(scalars + 32 * (size_t)i));
+    BPG_HIP(hipMemcpyAsync(ws.small.p, s.data(), (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, ws.st));
+    // compressed points -> device decompress
+    ws.gh.grow((size_t)n * 32 + 64);
+    BPG_HIP(hipMemcpyAsync(ws.gh.p, points, (size_t)n * 32, hipMemcpyHostToDevice, ws.st));
+    int one = 1;
+    BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, ws.st));
+    launch_decompress(as<uint32_t>(ws.gh), as<PtD>(ws.pts), as<int>(ws.okflag), n, ws.st);
+    int ok = 0;
+    BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, ws.st));
+    MsmSeg seg{as<ScD>(ws.small), as<PtD>(ws.pts), n, 0};
+    MsmPlan p = ws.msm->enqueue(&seg, 1, 1, ws.rows_host);
+    BPG_HIP(hipStreamSynchronize(ws.st));
+    if (!ok) return -1;
+    Point r;
+    combine_rows(r, ws.rows_host, p.W, p.c);
+    ristretto_compress(out, r);
+    return 0;
+}
+
+// Upload base^(2^b) (b < 40) in Montgomery form; returns device pointer.
+static ScD *upload_base2(Workspace &ws, int slot, const Scalar &base) {
+    ScD *h = ws.small_host + 40 * slot;
+    Scalar cur = base;
+    for (int b = 0; b < 40; b++) { h[b] = mont(cur); cur = cur * cur; }
+    ScD *d = as<ScD>(ws.tabs) + 40 * slot;
+    BPG_HIP(hipMemcpyAsync(d, h, 40 * sizeof(ScD), hipMemcpyHostToDevice, ws.st));
+    return d;
+}
+// out[i] = mont(base^i), i < count, via two 1024-ary levels
+static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t count, DBuf &lo, DBuf &hi, ScD *out) {
+    uint32_t nhi = count / 1024 + 1;
+    lo.grow(1024 * sizeof(ScD));
+    hi.grow((size_t)nhi * sizeof(ScD));
+    ScD *b2 = upload_base2(ws, slot, base);
+    ScD *b2h = upload_base2(ws, slot + 1, sc_pow_u64(base, 1024));
+    launch_pow_table(b2, 0, 1024, as<ScD>(lo), ws.st);
+    launch_pow_table(b2h, 0, nhi, as<ScD>(hi), ws.st);
+    if (out) launch_pow_expand(as<ScD>(lo), as<ScD>(hi), count, out, ws.st);
+}
+
+static void check_point_nonidentity(const uint8_t c[32]) { (void)c; }
+
+// ------------------------------------------------------------------- prove
+std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
+                               const uint8_t entropy[32], ProveTimings *tm) {
+    if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
+    DeviceContext &ctx = DeviceContext::get(cs.device);
+    const uint32_t n = cs.n, m = cs.m, N = cs.N, lgN = cs.lgN;
+    ctx.ensure_gens(N);
+    Workspace &ws = thread_workspace(cs.device);
+    hipStream_t st = ws.st;
+    double t0 = now_ms();
+    ws.tabs.grow(8 * 40 * sizeof(ScD));
+
+    // transcript prefix: Transcript::new(label) + Prover::new + commit(V_i)
+    Transcript T(label, label_len);
+    T.append_message("dom-sep", (const uint8_t *)"r1cs v1", 7);
+    for (uint32_t i = 0; i < m; i++) T.append_point("V", cs.V.data() + 32 * (size_t)i);
+    T.append_u64("m", m);
+    TranscriptRng rng(T);
+    for (uint32_t i = 0; i < m; i++) rng.rekey_with_witness_bytes("v_blinding", (const uint8_t *)cs.vb[i].v, 32);
+    rng.finalize(entropy);
+    Scalar i_bl = rng.random_scalar(), o_bl = rng.random_scalar(), s_bl = rng.random_scalar();
+
+    // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G> (blinding terms added on the host)
+    PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
+    MsmPlan pA{}, pS{};
+    if (n) {
+        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), ctx.G, n, 0},
+                          {as<ScD>(const_cast<DBuf &>(cs.aR)), ctx.H, n, 0},
+                          {as<ScD>(const_cast<DBuf &>(cs.aO)), ctx.G, n, 1}};
+        pA = ws.msm->enqueue(segA, 3, 2, rowsA);
+    }
+    // s_L, s_R: 2n serial TranscriptRng draws (one Keccak-f each) overlap the MSM
+    double t_rng0 = now_ms();
+    ws.stage(2 * (size_t)n * 32 + 64);
+    ScD *sh = reinterpret_cast<ScD *>(ws.s_host);
+    for (uint32_t i = 0; i < 2 * n; i++) sh[i] = to_dev(rng.random_scalar());
+    double t_rng1 = now_ms();
+    ws.sL.grow((size_t)n * sizeof(ScD) + 64);
+    ws.sR.grow((size_t)n * sizeof(ScD) + 64);
+    if (n) {
+        BPG_HIP(hipMemcpyAsync(ws.sL.p, sh, (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, st));
+        BPG_HIP(hipMemcpyAsync(ws.sR.p, sh + n, (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, st));
+        MsmSeg segS[2] = {{as<ScD>(ws.sL), ctx.G, n, 0}, {as<ScD>(ws.sR), ctx.H, n, 0}};
+        pS = ws.msm->enqueue(segS, 2, 1, rowsS);
+    }
+    BPG_HIP(hipStreamSynchronize(st));
+    Point AI, AO, S, tmp;
+    if (n) {
+        combine_rows(AI, rowsA, pA.W, pA.c);
+        combine_rows(AO, rowsA + pA.W, pA.W, pA.c);
+        combine_rows(S, rowsS, pS.W, pS.c);
+    } else {
+        pt_identity(AI); pt_identity(AO); pt_identity(S);
+    }
+    mul_B_blinding(tmp, i_bl); pt_add(AI, AI, tmp);
+    mul_B_blinding(tmp, o_bl); pt_add(AO, AO, tmp);
+    mul_B_blinding(tmp, s_bl); pt_add(S, S, tmp);
+    uint8_t cAI[32], cAO[32], cS[32];
+    ristretto_compress(cAI, AI); ristretto_compress(cAO, AO); ristretto_compress(cS, S);
+    T.append_point("A_I1", cAI);
+    T.append_point("A_O1", cAO);
+    T.append_point("S1", cS);
+    T.append_message("dom-sep", (const uint8_t *)"r1cs-1phase", 11);
+    const uint8_t zero32[32] = {0};
+    T.append_point("A_I2", zero32);
+    T.append_point("A_O2", zero32);
+    T.append_point("S2", zero32);
+    Scalar y = T.challenge_scalar("y"), z = T.challenge_scalar("z");
+    double t1 = now_ms();
+
+    // vectors: powers, flattened_constraints(z), l(x)/r(x) coefficients, t(x)
+    Scalar y_inv = sc_invert(y);
+    ws.ypm.grow((size_t)N * sizeof(ScD));
+    ws.yipm.grow((size_t)N * sizeof(ScD));
+    DBuf &lo1 = ws.zlo, &hi1 = ws.zhi;
+    pow_vector(ws, 0, y, N, lo1, hi1, as<ScD>(ws.ypm));
+    // second set of tables for y^-1 uses gh as temp space for the hi level
+    ws.gh.grow(std::max<size_t>((size_t)(N / 1024 + 2) * sizeof(ScD), 64));
+    {
+        DBuf lo2, hi2;
+        pow_vector(ws, 2, y_inv, N, lo2, hi2, as<ScD>(ws.yipm));
+        pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);   // also syncs tables below
+        BPG_HIP(hipStreamSynchronize(st));
+        if (lo2.p) (void)hipFree(lo2.p);
+        if (hi2.p) (void)hipFree(hi2.p);
+    }
+    ws.w.grow((size_t)cs.ncol * sizeof(ScD) + 64);
+    CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
+               as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
+               as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
+    launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
+    ScD *wL = as<ScD>(ws.w), *wR = wL + n, *wO = wL + 2 * (size_t)n, *wV = wL + 3 * (size_t)n;
+    for (DBuf *d : {&ws.l1, &ws.r0, &ws.r1, &ws.r3}) d->grow((size_t)n * sizeof(ScD) + 64);
+    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    ws.small.grow(64 * sizeof(ScD));
+    ScD *dsmall = as<ScD>(ws.small);
+    if (n) {
+        launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(ws.sR), wL, wR,
+                        wO, as<ScD>(ws.ypm), as<ScD>(ws.yipm), n, as<ScD>(ws.l1), as<ScD>(ws.r0), as<ScD>(ws.r1),
+                        as<ScD>(ws.r3), st);
+        launch_tpoly(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0),
+                     as<ScD>(ws.r1), as<ScD>(ws.r3), n, as<ScD>(ws.partial), dsmall, st);
+    } else {
+        BPG_HIP(hipMemsetAsync(dsmall, 0, 6 * sizeof(ScD), st));
+    }
+    if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(ws.partial), dsmall + 6, st);
+    else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
+    BPG_HIP(hipMemcpyAsync(ws.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
+    BPG_HIP(hipStreamSynchronize(st));
+    Scalar tp[6];
+    for (int k = 0; k < 6; k++) tp[k] = from_dev(ws.small_host[1000 + k]);
+    Scalar tb2 = from_dev(ws.small_host[1006]);
+    Scalar tb1 = rng.random_scalar(), tb3 = rng.random_scalar(), tb4 = rng.random_scalar(), tb5 = rng.random_scalar(),
+           tb6 = rng.random_scalar();
+    uint8_t cT[5][32];
+    pedersen_commit(cT[0], tp[0], tb1);
+    pedersen_commit(cT[1], tp[2], tb3);
+    pedersen_commit(cT[2], tp[3], tb4);
+    pedersen_commit(cT[3], tp[4], tb5);
+    pedersen_commit(cT[4], tp[5], tb6);
+    T.append_point("T_1", cT[0]);
+    T.append_point("T_3", cT[1]);
+    T.append_point("T_4", cT[2]);
+    T.append_point("T_5", cT[3]);
+    T.append_point("T_6", cT[4]);
+    Scalar u = T.challenge_scalar("u"), x = T.challenge_scalar("x");
+    auto eval6 = [&](const Scalar c[6]) {
+        Scalar acc = x * c[5];
+        for (int k = 4; k >= 0; k--) acc = x * (c[k] + acc);
+        return acc;
+    };
+    Scalar tbs[6] = {tb1, tb2, tb3, tb4, tb5, tb6};
+    Scalar t_x = eval6(tp), t_xb = eval6(tbs);
+    Scalar e_bl = x * (i_bl + x * (o_bl + x * s_bl));
+    T.append_scalar("t_x", t_x);
+    T.append_scalar("t_x_blinding", t_xb);
+    T.append_scalar("e_blinding", e_bl);
+    Scalar wch = T.challenge_scalar("w");
+    Point Qp; mul_B(Qp, wch);
+    ws.Q.grow(sizeof(PtD));
+    PtD Qd; pt_to_dev(Qd.v, Qp);
+    BPG_HIP(hipMemcpyAsync(ws.Q.p, &Qd, sizeof(PtD), hipMemcpyHostToDevice, st));
+    ws.a.grow((size_t)N * sizeof(ScD) + 64);
+    ws.b.grow((size_t)N * sizeof(ScD) + 64);
+    launch_lr_eval(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0), as<ScD>(ws.r1),
+                   as<ScD>(ws.r3), as<ScD>(ws.ypm), n, N, mont(x), mont(x * x), as<ScD>(ws.a), as<ScD>(ws.b), st);
+    double t2 = now_ms();
+
+    // InnerProductProof::create with weighted single-scalar point folding
+    T.append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
+    T.append_u64("n", N);
+    std::vector<uint8_t> LRc(64 * (size_t)lgN);
+    Scalar lam = Scalar::one(), mu = Scalar::one();
+    const PtD *Gh = ctx.G, *Hh = ctx.H;
+    ws.mscal.grow((size_t)(2 * N + 2) * sizeof(ScD) + 64);
+    if (N >= 2) {
+        for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(N / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(N / 2) * sizeof(PtD)); }
+    }
+    uint32_t len = N;
+    for (uint32_t k = 0; len != 1; k++) {
+        const uint32_t h = len / 2;
+        IppRoundArgs A;
+        A.h = h; A.n = n;
+        A.lamG1 = mont(lam); A.lamGu = mont(lam * u);
+        A.muH1 = mont(mu); A.muHu = mont(mu * u);
+        ScD *ms = as<ScD>(ws.mscal);
+        launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
+        const PtD *Qdev = as<PtD>(ws.Q);
+        MsmSeg seg[6] = {{ms, Gh + h, h, 0}, {ms + h, Hh, h, 0}, {ms + 4 * (size_t)h, Qdev, 1, 0},
+                         {ms + 2 * (size_t)h, Gh, h, 1}, {ms + 3 * (size_t)h, Hh + h, h, 1},
+                         {ms + 4 * (size_t)h + 1, Qdev, 1, 1}};
+        MsmPlan pl = ws.msm->enqueue(seg, 6, 2, rowsLR);
+        BPG_HIP(hipStreamSynchronize(st));
+        Point Lp, Rp;
+        combine_rows(Lp, rowsLR, pl.W, pl.c);
+        combine_rows(Rp, rowsLR + pl.W, pl.W, pl.c);
+        uint8_t *cl = LRc.data() + 64 * (size_t)k, *cr = cl + 32;
+        ristretto_compress(cl, Lp);
+        ristretto_compress(cr, Rp);
+        T.append_point("L", cl);
+        T.append_point("R", cr);
+        Scalar uk = T.challenge_scalar("u");
+        Scalar uinv = sc_invert(uk);
+        launch_ipp_fold_scalars(as<ScD>(ws.a), as<ScD>(ws.b), h, mont(uk), mont(uinv), st);
+        if (h > 1) {
+            Scalar u2 = uk * uk, ui2 = uinv * uinv;
+            Scalar yh = sc_pow_u64(y_inv, h);
+            Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
+            PtD *Gn = as<PtD>(ws.Gp[k & 1]), *Hn = as<PtD>(ws.Hp[k & 1]);
+            launch_ipp_fold_points(Gh, Hh, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn, st);
+            Gh = Gn; Hh = Hn;
+        }
+        lam = lam * uinv;
+        mu = mu * uk;
+        len = h;
+    }
+    BPG_HIP(hipMemcpyAsync(ws.small_host + 1010, ws.a.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    BPG_HIP(hipMemcpyAsync(ws.small_host + 1011, ws.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    BPG_HIP(hipStreamSynchronize(st));
+    Scalar fa = from_dev(ws.small_host[1010]), fb = from_dev(ws.small_host[1011]);
+    double t3 = now_ms();
+
+    // R1CSProof::to_bytes (one-phase)
+    std::vector<uint8_t> proof;
+    proof.reserve(417 + 64 * (size_t)lgN);
+    proof.push_back(0);
+    auto put = [&](const uint8_t *p) { proof.insert(proof.end(), p, p + 32); };
+    put(cAI); put(cAO); put(cS);
+    for (int i = 0; i < 5; i++) put(cT[i]);
+    uint8_t b32[32];
+    t_x.to_bytes(b32); put(b32);
+    t_xb.to_bytes(b32); put(b32);
+    e_bl.to_bytes(b32); put(b32);
+    proof.insert(proof.end(), LRc.begin(), LRc.end());
+    fa.to_bytes(b32); put(b32);
+    fb.to_bytes(b32); put(b32);
+    ProveTimings t;
+    t.rng_ms = t_rng1 - t_rng0;
+    t.commit_ms = t1 - t0;
+    t.vec_ms = t2 - t1;
+    t.ipp_ms = t3 - t2;
+    t.total_ms = t3 - t0;
+    last_timings() = t;
+    if (tm) *tm = t;
+    (void)check_point_nonidentity;
+    return proof;
+}
+
+// ------------------------------------------------------------------ verify
+int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V, const uint8_t *proof,
+               size_t plen, const uint8_t entropy[32]) {
+    DeviceContext &ctx = DeviceContext::get(cs.device);
+    const uint32_t n = cs.n, m = cs.m, N = cs.N;
+    // R1CSProof::from_bytes
+    if (plen < 1 || proof[0] != 0) return 0;
+    const uint8_t *p = proof + 1;
+    size_t rem = plen - 1;
+    if (rem % 32 != 0 || rem < 11 * 32) return 0;
+    const uint8_t *cAI = p, *cAO = p + 32, *cS = p + 64, *cT = p + 96;
+    Scalar tx, txb, ebl, pa, pb;
+    if (!Scalar::from_canonical(p + 256, tx) || !Scalar::from_canonical(p + 288, txb) ||
+        !Scalar::from_canonical(p + 320, ebl))
+        return 0;
+    const uint8_t *ipp = p + 352;
+    size_t ne = (rem - 352) / 32;
+    if (ne < 2 || (ne - 2) % 2) return 0;
+    uint32_t lgn = (uint32_t)((ne - 2) / 2);
+    if (lgn >= 32) return 0;
+    if (!Scalar::from_canonical(ipp + 64 * lgn, pa) || !Scalar::from_canonical(ipp + 64 * lgn + 32, pb)) return 0;
+    if (N != (1u << lgn)) return 0;
+    ctx.ensure_gens(N);
+    Workspace &ws = thread_workspace(cs.device);
+    hipStream_t st = ws.st;
+    ws.tabs.grow(8 * 40 * sizeof(ScD));
+    auto is_zero32 = [](const uint8_t *b) { uint8_t a = 0; for (int i = 0; i < 32; i++) a |= b[i]; return a == 0; };
+
+    Transcript T(label, label_len);
+    T.append_message("dom-sep", (const uint8_t *)"r1cs v1", 7);
+    for (uint32_t i = 0; i < m; i++) T.append_point("V", V + 32 * (size_t)i);
+    T.append_u64("m", m);
+    if (is_zero32(cAI) || is_zero32(cAO) || is_zero32(cS)) return 0;
+    T.append_point("A_I1", cAI);
+    T.append_point("A_O1", cAO);
+    T.append_point("S1", cS);
+    T.append_message("dom-sep", (const uint8_t *)"r1cs-1phase", 11);
+    const uint8_t zero32[32] = {0};
+    T.append_point("A_I2", zero32);
+    T.append_point("A_O2", zero32);
+    T.append_point("S2", zero32);
+    Scalar y = T.challenge_scalar("y"), z = T.challenge_scalar("z");
+    static const char *TL[5] = {"T_1", "T_3", "T_4", "T_5", "T_6"};
+    for (int i = 0; i < 5; i++) {
+        if (is_zero32(cT + 32 * i)) return 0;
+        T.append_point(TL[i], cT + 32 * i);
+    }
+    Scalar u = T.challenge_scalar("u"), x = T.challenge_scalar("x");
+    T.append_message("t_x", p + 256, 32);
+    T.append_message("t_x_blinding", p + 288, 32);
+    T.append_message("e_blinding", p + 320, 32);
+    Scalar w = T.challenge_scalar("w");
+    // device: flattened_constraints(z), y^-i
+    Scalar y_inv = sc_invert(y);
+    ws.yipm.grow((size_t)N * sizeof(ScD));
+    {
+        DBuf lo2, hi2;
+        pow_vector(ws, 2, y_inv, N, lo2, hi2, as<ScD>(ws.yipm));
+        pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);
+        BPG_HIP(hipStreamSynchronize(st));
+        if (lo2.p) (void)hipFree(lo2.p);
+        if (hi2.p) (void)hipFree(hi2.p);
+    }
+    ws.w.grow((size_t)cs.ncol * sizeof(ScD) + 64);
+    CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
+               as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
+               as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
+    launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
+    // verification_scalars
+    T.append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
+    T.append_u64("n", N);
+    std::vector<Scalar> uc(lgn), ucinv;
+    for (uint32_t k = 0; k < lgn; k++) {
+        if (is_zero32(ipp + 64 * k) || is_zero32(ipp + 64 * k + 32)) return 0;
+        T.append_point("L", ipp + 64 * k);
+        T.append_point("R", ipp + 64 * k + 32);
+        uc[k] = T.challenge_scalar("u");
+    }
+    ucinv = uc;
+    sc_batch_invert(ucinv);
+    Scalar allinv = Scalar::one();
+    for (auto &v : ucinv) allinv = allinv * v;
+    std::vector<Scalar> u2(lgn), ui2(lgn);
+    for (uint32_t k = 0; k < lgn; k++) { u2[k] = uc[k] * uc[k]; ui2[k] = ucinv[k] * ucinv[k]; }
+    TranscriptRng rng(T);
+    rng.finalize(entropy);
+    Scalar r = rng.random_scalar();
+    Scalar xx = x * x, rxx = r * xx, xxx = x * xx;
+    // g, h scalars on device
+    ScD *u2h = ws.small_host + 2000;
+    for (uint32_t k = 0; k < lgn; k++) u2h[k] = mont(u2[k]);
+    ws.small.grow(64 * sizeof(ScD) + 4096 * sizeof(ScD));
+    ScD *u2d = as<ScD>(ws.small);
+    if (lgn) BPG_HIP(hipMemcpyAsync(u2d, u2h, lgn * sizeof(ScD), hipMemcpyHostToDevice, st));
+    ws.gh.grow((size_t)2 * N * sizeof(ScD) + 64);
+    ws.ynwR.grow((size_t)(n ? n : 1) * sizeof(ScD) + 64);
+    launch_verify_gh(as<ScD>(ws.w), as<ScD>(ws.yipm), u2d, to_dev(allinv), n, N, lgn, mont(x), mont(pa), mont(pb),
+                     mont(u), as<ScD>(ws.gh), as<ScD>(ws.ynwR), st);
+    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    ScD *dsm = u2d + 40;
+    if (n) launch_dot(as<ScD>(ws.ynwR), as<ScD>(ws.w), n, as<ScD>(ws.partial), dsm, st);
+    else BPG_HIP(hipMemsetAsync(dsm, 0, sizeof(ScD), st));
+    // wV and wc back to the host
+    ScD *hsm = ws.small_host + 2100;
+    BPG_HIP(hipMemcpyAsync(hsm, dsm, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    std::vector<ScD> wvh(m + 1);
+    BPG_HIP(hipMemcpyAsync(wvh.data(), as<ScD>(ws.w) + 3 * (size_t)n, (size_t)(m + 1) * sizeof(ScD),
+                           hipMemcpyDeviceToHost, st));
+    // small points: A_I1, A_O1, S1, V_i, T_*, L_k, R_k
+    const uint32_t ns = 3 + m + 5 + 2 * lgn;
+    std::vector<uint8_t> comp((size_t)ns * 32);
+    memcpy(comp.data(), cAI, 32); memcpy(comp.data() + 32, cAO, 32); memcpy(comp.data() + 64, cS, 32);
+    if (m) memcpy(comp.data() + 96, V, (size_t)m * 32);
+    memcpy(comp.data() + 96 + 32 * (size_t)m, cT, 160);
+    for (uint32_t k = 0; k < lgn; k++) {
+        memcpy(comp.data() + (8 + m + k) * (size_t)32, ipp + 64 * k, 32);
+        memcpy(comp.data() + (8 + m + lgn + k) * (size_t)32, ipp + 64 * k + 32, 32);
+    }
+    ws.pts.grow((size_t)ns * sizeof(PtD) + 64);
+    ws.okflag.grow(64);
+    ws.mscal.grow((size_t)ns * 32 + (size_t)ns * sizeof(ScD) + 64);
+    uint32_t *compd = as<uint32_t>(ws.mscal);
+    ScD *sscal = reinterpret_cast<ScD *>(as<uint8_t>(ws.mscal) + (size_t)ns * 32);
+    BPG_HIP(hipMemcpyAsync(compd, comp.data(), comp.size(), hipMemcpyHostToDevice, st));
+    int one = 1;
+    BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
+    launch_decompress(compd, as<PtD>(ws.pts), as<int>(ws.okflag), ns, st);
+    int ok = 0;
+    BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, st));
+    BPG_HIP(hipStreamSynchronize(st));
+    if (!ok) return 0;
+    Scalar delta = from_dev(hsm[0]);
+    Scalar wc = from_dev(wvh[m]);
+    std::vector<ScD> ss(ns);
+    ss[0] = to_dev(x); ss[1] = to_dev(xx); ss[2] = to_dev(xxx);
+    for (uint32_t i = 0; i < m; i++) ss[3 + i] = to_dev(from_dev(wvh[i]) * rxx);
+    Scalar Ts[5] = {r * x, rxx * x, rxx * xx, rxx * xxx, rxx * xx * xx};
+    for (int i = 0; i < 5; i++) ss[3 + m + i] = to_dev(Ts[i]);
+    for (uint32_t k = 0; k < lgn; k++) { ss[8 + m + k] = to_dev(u2[k]); ss[8 + m + lgn + k] = to_dev(ui2[k]); }
+    BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
+    MsmSeg seg[3] = {{as<ScD>(ws.gh), ctx.G, N, 0}, {as<ScD>(ws.gh) + N, ctx.H, N, 0}, {sscal, as<PtD>(ws.pts), ns, 0}};
+    MsmPlan pl = ws.msm->enqueue(seg, 3, 1, ws.rows_host);
+    BPG_HIP(hipStreamSynchronize(st));
+    Point R;
+    combine_rows(R, ws.rows_host, pl.W, pl.c);
+    // B and B_blinding terms
+    Scalar sB = w * (tx - pa * pb) + r * (xx * (wc + delta) - tx);
+    Scalar sBb = -ebl - r * txb;
+    Point t1, t2;
+    mul_B(t1, sB); mul_B_blinding(t2, sBb);
+    pt_add(R, R, t1); pt_add(R, R, t2);
+    return pt_is_identity(R) ? 1 : 0;
+}
+
+}  // namespace bpg

@@ -64,6 +64,10 @@ void free_proof(struct ProofArtifacts *artifacts);
 /* Added: thread-local description of the last error ("" if none). */
 const char *bpg_last_error(void);
 
+/* Added: `prover.num_constraints()` of the last c_prove on this thread
+ * (the reference prints it from prove.rs:75; the CLI prints it here). */
+uint64_t bpg_last_num_constraints(void);
+
 /* Added: deterministic mode. Every `thread_rng()` draw of the reference
  * (commitment blindings gadget.rs:32, commitments.rs:28,40 and the 32-byte
  * TranscriptRng finalize entropy inside Prover::prove / Verifier::verify)
@@ -171,14 +175,22 @@ int bpg_last_timings(double *out, int n);
 int bpg_msm(bpg_ctx *ctx, const uint8_t *scalars, const uint8_t *points,
             uint32_t count, uint8_t out[32]);
 
-/* Statement synthesis only (no proof): runs the prover-side driver of
- * prove.rs:37-75 under the current seed and exports the flattened system.
- * Buffers are owned by the returned handle. */
+/* Statement synthesis only (no device work): runs the prover-side driver of
+ * prove.rs:37-75 (commitment blindings drawn from the calling thread's
+ * entropy source, so bpg_set_seed first for reproducible output) and exports
+ * the flattened system. bpg_synth_commitments returns the `.coms` NAMES in
+ * commit order, one per line (the points themselves need the device:
+ * bpg_pedersen_commit). Buffers are owned by the returned handle. */
 typedef struct bpg_synth bpg_synth;
 bpg_synth *bpg_synthesize(const char *instance, const char *witness,
                           const char *gadgets);
+/* Verifier side (verify.rs:36-69): commitments parsed from `.coms` text. */
+bpg_synth *bpg_synthesize_verifier(const char *instance, const char *commitments,
+                                   const char *gadgets);
 const bpg_r1cs_view *bpg_synth_view(const bpg_synth *s);
 const char *bpg_synth_commitments(const bpg_synth *s);
+/* Verifier-side commitments (m x 32 bytes, commit order). */
+const uint8_t *bpg_synth_V(const bpg_synth *s);
 void bpg_synth_free(bpg_synth *s);
 
 #ifdef __cplusplus

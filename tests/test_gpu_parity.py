@@ -1,0 +1,160 @@
+"""Device parity tests (MI355X): HIP path through the C-ABI vs the CPU oracle.
+
+All comparisons are bit-exact (integer/byte work). Sizes here keep the oracle
+within seconds; full-size properties are in test_gpu_scale.py.
+"""
+import os
+import random
+
+import pytest
+
+import oracle as O
+import synth as S
+from conftest import read_fixture
+
+pytestmark = pytest.mark.gpu
+
+L = S.L
+
+
+@pytest.fixture(scope="module")
+def bpg():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bpg", os.path.join(root, "bulletproof-gadgets_amd", "bpg.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="module")
+def ctx(bpg):
+    return bpg.Context(0)
+
+
+def rand_points(rnd, k):
+    return [O.from_uniform(bytes(rnd.getrandbits(8) for _ in range(64))) for _ in range(k)]
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 64, 191, 1000, 5000])
+def test_msm_random(ctx, n):
+    rnd = random.Random(n)
+    pts = rand_points(rnd, min(n, 64))
+    pts = [pts[i % len(pts)] for i in range(n)]
+    sc = [rnd.randrange(L).to_bytes(32, "little") for _ in range(n)]
+    assert ctx.msm(sc, pts) == O.msm(sc, pts)
+
+
+def test_msm_structured_scalars(ctx):
+    # bits / small values / zeros / l-1 / non-canonical inputs: skewed buckets
+    rnd = random.Random(3)
+    n = 3000
+    pts = rand_points(rnd, 50)
+    pts = [pts[i % 50] for i in range(n)]
+    vals = []
+    for i in range(n):
+        k = i % 6
+        v = [0, 1, rnd.randrange(2), L - 1, rnd.randrange(1 << 64), (1 << 256) - 1 - i][k]
+        vals.append(v.to_bytes(32, "little"))
+    assert ctx.msm(vals, pts) == O.msm(vals, pts)
+    ones = [(1).to_bytes(32, "little")] * 4096
+    same = [pts[0]] * 4096
+    assert ctx.msm(ones, same) == O.msm(ones, same)
+
+
+def test_msm_identity_and_invalid(ctx, bpg):
+    assert ctx.msm([b"\0" * 32], [O.pedersen_gens()[0]]) == b"\0" * 32
+    with pytest.raises(bpg.BpgError):
+        ctx.msm([b"\1" + b"\0" * 31], [b"\xff" * 32])
+
+
+def test_pedersen(ctx):
+    rnd = random.Random(11)
+    v = [rnd.getrandbits(255).to_bytes(32, "little") for _ in range(70)]    # from_bits: may exceed l
+    vb = [rnd.randrange(L).to_bytes(32, "little") for _ in range(70)]
+    got = ctx.pedersen(v, vb)
+    for a, b, g in zip(v, vb, got):
+        assert g == O.pedersen_commit(a, b)
+
+
+def test_range_proof_inner_abi(ctx):
+    x = S.be_to_scalar(bytes([0x05, 0x22, 0xa6, 0x4d, 0x7b, 0x93, 0x1e]))
+    for n, ok in [(56, True), (48, False)]:
+        cs = S.Cs(True)
+        S.range_proof(cs, S.lc_const(x), n, x)
+        flat = cs.to_flat()
+        ent = bytes(range(32))
+        proof, _ = ctx.r1cs_prove(b"RangeProof", flat.view(), ent)
+        o_proof, _ = O.r1cs_prove(b"RangeProof", flat, ent)
+        assert proof == o_proof
+        vcs = S.Cs(False)
+        S.range_proof(vcs, S.lc_const(x), n, None)
+        vflat = vcs.to_flat()
+        assert ctx.r1cs_verify(b"RangeProof", vflat.view(secrets=False), [], proof) == ok
+        assert O.r1cs_verify(b"RangeProof", vflat, [], proof) == (1 if ok else 0)
+
+
+FIXTURES = ["bounds_check", "equality", "inequality", "less_than", "or3", "or5", "or", "example"]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fixture_bit_exact(bpg, resources, name):
+    fx = read_fixture(os.path.join(resources, name))
+    seed = 77 + len(name)
+    bpg.set_seed(seed)
+    proof, coms = bpg.prove(name, fx["inst"], fx["wtns"], fx["gadgets"])
+    o_proof, o_coms, flat = S.prove_statement(name.encode(), fx["inst"], fx["wtns"], fx["gadgets"], seed)
+    assert coms == o_coms
+    assert proof == o_proof
+    assert bpg.verify(name, fx["inst"], proof, coms, fx["gadgets"])
+    assert S.verify_statement(name.encode(), fx["inst"], proof, coms, fx["gadgets"])
+
+
+@pytest.mark.parametrize("name", ["bounds_check", "less_than", "example"])
+def test_fixture_rejects(bpg, resources, name):
+    fx = read_fixture(os.path.join(resources, name))
+    bpg.set_seed(5)
+    proof, coms = bpg.prove(name, fx["inst"], fx["wtns"], fx["gadgets"])
+    assert not bpg.verify(name + "x", fx["inst"], proof, coms, fx["gadgets"])        # label is bound
+    for pos in (1, 100, 300, len(proof) - 70, len(proof) - 1):
+        bad = bytearray(proof)
+        bad[pos] ^= 0x10
+        assert not bpg.verify(name, fx["inst"], bytes(bad), coms, fx["gadgets"])
+    assert not bpg.verify(name, fx["inst"], proof[:-32], coms, fx["gadgets"])
+    lines = coms.splitlines()
+    lines[0], lines[1] = lines[1], lines[0]
+    assert not bpg.verify(name, fx["inst"], proof, "\n".join(lines) + "\n", fx["gadgets"])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["mimc_hash", "merkle_tree", "set_membership", "or2", "or4"])
+def test_fixture_bit_exact_large(bpg, resources, name):
+    test_fixture_bit_exact(bpg, resources, name)
+
+
+def test_unsatisfied_statement_rejected(bpg, resources):
+    # less_than.wtns witnesses with the operands swapped: the circuit is not
+    # satisfied, the proof must not verify (reference less_than tests)
+    fx = read_fixture(os.path.join(resources, "less_than"))
+    g = fx["gadgets"].splitlines()
+    swapped = []
+    for line in g:
+        t = line.split()
+        swapped.append(" ".join([t[0], t[2], t[1]]) if t and t[0] == "LESS_THAN" else line)
+    gad = "\n".join(swapped)
+    bpg.set_seed(1)
+    proof, coms = bpg.prove("lt", fx["inst"], fx["wtns"], gad)
+    assert not bpg.verify("lt", fx["inst"], proof, coms, gad)
+
+
+def test_prepared_batch_matches_single(bpg, ctx, resources):
+    fx = read_fixture(os.path.join(resources, "or5"))
+    bpg.set_seed(2)
+    syn = bpg.Synth(fx["inst"], fx["wtns"], fx["gadgets"])
+    prep = ctx.prepare(syn.view)
+    ents = [bytes([k]) * 32 for k in range(6)]
+    proofs = prep.prove_batch(b"batch", ents, threads=3)
+    for k, p in enumerate(proofs):
+        single, _ = ctx.r1cs_prove(b"batch", syn.view, ents[k])
+        assert p == single
+    assert len(set(proofs)) == 6

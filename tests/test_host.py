@@ -1,0 +1,102 @@
+"""CPU-side checks of the product library (no GPU compute calls):
+exports, statement synthesis parity with the oracle's mirror of the
+reference circuit layer, error behaviour."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import synth as S
+from conftest import ROOT, read_fixture
+
+HEADER = os.path.join(ROOT, "include", "bpg.h")
+
+
+@pytest.fixture(scope="module")
+def bpg():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bpg", os.path.join(ROOT, "bulletproof-gadgets_amd", "bpg.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    if not os.path.exists(mod.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return mod
+
+
+def test_library_exports_every_header_symbol(bpg):
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(c_prove|c_verify|free_proof|bpg_[a-z_0-9]+)\s*\(", src))
+    assert names, "no declarations parsed"
+    lib = bpg.lib()
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+    assert set(bpg.EXPORTS) >= names
+
+
+ALL = ["bounds_check", "equality", "inequality", "less_than", "set_membership", "mimc_hash", "merkle_tree",
+       "or", "or2", "or3", "or4", "or5", "example"]
+
+
+@pytest.mark.parametrize("name", ALL)
+def test_synthesis_matches_oracle(bpg, resources, name):
+    fx = read_fixture(os.path.join(resources, name))
+    seed = 1234
+    bpg.set_seed(seed)
+    c = bpg.Synth(fx["inst"], fx["wtns"], fx["gadgets"])
+    st = S.synthesize_prover(fx["inst"], fx["wtns"], fx["gadgets"], seed=seed)
+    f = st.cs.to_flat()
+    assert (c.n, c.m, c.q) == (f.n, f.m, f.q)
+    assert c.vec("a_L", c.n) == f.a_L
+    assert c.vec("a_R", c.n) == f.a_R
+    assert c.vec("a_O", c.n) == f.a_O
+    assert c.vec("v", c.m) == f.v
+    assert c.vec("v_blinding", c.m) == f.v_blinding
+    assert c.rows() == f.rows
+    assert c.names() == st.com_order
+
+
+def test_verifier_synthesis_matches_oracle(bpg, resources):
+    fx = read_fixture(os.path.join(resources, "example"))
+    # any well-formed .coms file with the right names drives the verifier side
+    bpg.set_seed(1)
+    names = bpg.Synth(fx["inst"], fx["wtns"], fx["gadgets"]).names()
+    B = bytes.fromhex("e2f2ae0a6abc4e71a884a961c500515f58e30b6aa582dd8db6a65945e08d2d76")
+    coms = "".join("%s = 0x%s\n" % (n, B.hex()) for n in names)
+    c = bpg.Synth(fx["inst"], gadgets=fx["gadgets"], commitments=coms)
+    st = S.Statement(False, fx["inst"], fx["gadgets"], coms=coms)
+    f = st.cs.to_flat()
+    assert (c.n, c.m, c.q) == (f.n, f.m, f.q)
+    assert c.rows() == f.rows
+    assert c.V() == b"".join(st.cs.V)
+
+
+def test_mimc_gadget_block_is_1946_constraints(bpg):
+    # or_conjunction.rs:85 "HASH GADGET: 1946 Constraints": one-block preimage, padded
+    img = S.scalar_to_be(S.mimc_hash(b"\x43")).hex()
+    c = bpg.Synth("I0 = 0x%s\n" % img, "W0 = 0x43\n", "HASH I0 W0\n")
+    assert (c.n, c.q) == (972, 1946)
+
+
+@pytest.mark.parametrize("bad", [
+    ("I0 = 0x11\n", "W0 = 0x43\n", "FOO W0\n"),            # unknown gadget
+    ("I0 = 0x11\n", "W0 = 0x43\n", "BOUND W0 I0 I9\n"),    # missing instance
+    ("I0 = 0x1\n", "W0 = 0x43\n", "EQUALS W0 I0\n"),       # odd-length hex
+    ("I0 = 0x11\n", "W0 = 0x43\n", "\n"),                  # empty gadget line
+    ("", "W0 = 0x43\n", "OR\n"),                           # unexpected end of input
+])
+def test_synthesis_errors_are_reported(bpg, bad):
+    with pytest.raises(bpg.BpgError):
+        bpg.Synth(*bad)
+
+
+def test_product_fails_loudly_without_device(bpg, resources):
+    if os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES") != "":
+        pytest.skip("a HIP device may be present")
+    fx = read_fixture(os.path.join(resources, "bounds_check"))
+    with pytest.raises(bpg.BpgError, match="no HIP device"):
+        bpg.prove("x", fx["inst"], fx["wtns"], fx["gadgets"])
+    assert not bpg.verify("x", fx["inst"], b"\0" * 417, "", fx["gadgets"])
+    assert "no HIP device" in bpg.last_error()
