@@ -69,10 +69,10 @@ def lib():
         L.bpg_ctx_destroy.argtypes = [vp]
         L.bpg_gens_ensure.argtypes = [vp, u32]
         L.bpg_pedersen_commit.argtypes = [vp, vp, vp, u32, vp]
-        L.bpg_r1cs_prove.argtypes = [vp, vp, sz, ctypes.POINTER(R1csView), vp, vp, sz, ctypes.POINTER(sz), vp]
-        L.bpg_r1cs_verify.argtypes = [vp, vp, sz, ctypes.POINTER(R1csView), vp, vp, sz, vp]
+        L.bpg_r1cs_prove.argtypes = [vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz), vp]
+        L.bpg_r1cs_verify.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp]
         L.bpg_prepare.restype = vp
-        L.bpg_prepare.argtypes = [vp, ctypes.POINTER(R1csView)]
+        L.bpg_prepare.argtypes = [vp, vp]
         L.bpg_prepared_free.argtypes = [vp]
         L.bpg_prove_batch.argtypes = [vp, vp, sz, vp, u32, u32, vp, sz, ctypes.POINTER(sz)]
         L.bpg_last_timings.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
@@ -195,11 +195,12 @@ class Context:
             raise BpgError(last_error())
         return [out.raw[32 * i:32 * i + 32] for i in range(len(v))]
 
+    # `view` may be any ctypes mirror of bpg_r1cs_view (ours or the oracle's)
     def r1cs_prove(self, label, view, entropy):
         out = ctypes.create_string_buffer(MAX_PROOF)
         plen = ctypes.c_size_t(0)
         V = ctypes.create_string_buffer(32 * max(view.m, 1))
-        rc = lib().bpg_r1cs_prove(self.h, label, len(label), ctypes.byref(view), entropy, out, MAX_PROOF,
+        rc = lib().bpg_r1cs_prove(self.h, label, len(label), ctypes.addressof(view), entropy, out, MAX_PROOF,
                                   ctypes.byref(plen), V)
         if rc != 0:
             raise BpgError(last_error())
@@ -207,13 +208,13 @@ class Context:
 
     def r1cs_verify(self, label, view, V, proof, entropy=b"\x05" * 32):
         Vb = b"".join(V) or b"\0" * 32
-        rc = lib().bpg_r1cs_verify(self.h, label, len(label), ctypes.byref(view), Vb, proof, len(proof), entropy)
+        rc = lib().bpg_r1cs_verify(self.h, label, len(label), ctypes.addressof(view), Vb, proof, len(proof), entropy)
         if rc < 0:
             raise BpgError(last_error())
         return rc == 1
 
     def prepare(self, view):
-        p = lib().bpg_prepare(self.h, ctypes.byref(view))
+        p = lib().bpg_prepare(self.h, ctypes.addressof(view))
         if not p:
             raise BpgError(last_error())
         return Prepared(p)

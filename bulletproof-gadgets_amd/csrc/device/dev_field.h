@@ -10,10 +10,19 @@
 //     Montgomery (R = 2^256), no MFMA — this is 255-bit integer work.
 //   * points: extended twisted-Edwards (X:Y:Z:T), a = -1, 128 bytes.
 #pragma once
-#include <hip/hip_runtime.h>
 #include <stdint.h>
-
+#ifdef BPG_HOST_SIM
+// Host emulation build (tests/devsim): the same arithmetic compiled for the
+// CPU so it can be checked against Python big integers without a GPU.
+#define DEVI static inline
+#define __device__
+#define __constant__
+struct uint4 { uint32_t x, y, z, w; };
+static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
+#else
+#include <hip/hip_runtime.h>
 #define DEVI __device__ __forceinline__
+#endif
 
 struct fe { uint32_t v[8]; };
 struct sc { uint32_t v[8]; };

@@ -243,12 +243,22 @@ __global__ void k_fill_identity(ge *__restrict__ b, uint64_t n) {
     ge id; ge_identity(id);
     ge_store(b + i, id);
 }
+// After the chunk passes a key can still straddle chunk boundaries (short
+// runs); the entry that starts a run sums the rest of it and owns the bucket.
 __global__ void k_scatter(const uint32_t *__restrict__ keys, const ge *__restrict__ pts, const uint32_t *E_dev,
                           uint64_t cap, ge *__restrict__ buckets) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cap || i >= *E_dev) return;
-    ge p; ge_load(p, pts + i);
-    ge_store(buckets + keys[i], p);
+    uint64_t E = *E_dev;
+    if (i >= cap || i >= E) return;
+    uint32_t k = keys[i];
+    if (i > 0 && keys[i - 1] == k) return;
+    ge acc, p;
+    ge_load(acc, pts + i);
+    for (uint64_t j = i + 1; j < E && keys[j] == k; j++) {
+        ge_load(p, pts + j);
+        ge_add(acc, acc, p);
+    }
+    ge_store(buckets + k, acc);
 }
 // sum_{b in seg} (b+1) * S_b = acc + lo * run, with acc weights 1..seglen
 DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {
