@@ -307,4 +307,30 @@ const char *bpg_synth_commitments(const bpg_synth *s) { return s->names.c_str();
 const uint8_t *bpg_synth_V(const bpg_synth *s) { return s->s.cs->V().data(); }
 void bpg_synth_free(bpg_synth *s) { delete s; }
 
+int bpg_mimc_hash(const uint8_t *data, size_t len, uint8_t out[32]) {
+    return guarded([&]() -> int {
+        mimc_hash(std::vector<uint8_t>(data, data + len)).to_bytes(out);
+        return 0;
+    }, -1);
+}
+int bpg_mimc_sponge(const uint8_t *blocks, uint32_t count, uint8_t out[32]) {
+    return guarded([&]() -> int {
+        std::vector<Scalar> b(count);
+        for (uint32_t i = 0; i < count; i++) b[i] = Scalar::from_bits(blocks + 32 * (size_t)i);
+        mimc_sponge_native(b).to_bytes(out);
+        return 0;
+    }, -1);
+}
+
+int bpg_profile_enable(int on) { return set_kernel_profiling(on != 0); }
+int bpg_kernel_stats(const char *name, uint64_t *launches, double *total_ms, double *alg_bytes) {
+    KernelStat st;
+    if (!get_kernel_stat(name, st)) return -1;
+    *launches = st.launches;
+    *total_ms = st.total_ms;
+    *alg_bytes = st.alg_bytes;
+    return 0;
+}
+void bpg_kernel_stats_reset(void) { reset_kernel_stats(); }
+
 }  // extern "C"

@@ -6,6 +6,7 @@
 #include "r1cs_gpu.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <stdexcept>
@@ -88,6 +89,21 @@ void DeviceContext::ensure_gens(uint32_t N) {
     G = nG; H = nH; gens_cap = cap;
 }
 
+// ---------------------------------------------------------- instrumentation
+static std::atomic<bool> g_prof(false);
+static std::mutex g_prof_mu;
+static std::map<std::string, KernelStat> g_prof_stats;
+struct PendingEvent { const char *name; hipEvent_t a, b; double bytes; };
+int set_kernel_profiling(bool on) { g_prof = on; return 0; }
+bool get_kernel_stat(const char *name, KernelStat &out) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    auto it = g_prof_stats.find(name);
+    if (it == g_prof_stats.end()) return false;
+    out = it->second;
+    return true;
+}
+void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_stats.clear(); }
+
 // ---------------------------------------------------------------- workspace
 struct Workspace {
     int device = 0;
@@ -108,6 +124,34 @@ struct Workspace {
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
+    }
+    std::vector<PendingEvent> pend;
+    // bracket the launches issued between begin() and end() on `st`
+    int prof_begin(const char *name, double bytes) {
+        if (!g_prof) return -1;
+        PendingEvent e{name, nullptr, nullptr, bytes};
+        BPG_HIP(hipEventCreate(&e.a));
+        BPG_HIP(hipEventCreate(&e.b));
+        BPG_HIP(hipEventRecord(e.a, st));
+        pend.push_back(e);
+        return (int)pend.size() - 1;
+    }
+    void prof_end(int h) { if (h >= 0) BPG_HIP(hipEventRecord(pend[h].b, st)); }
+    void prof_flush() {   // call after the stream is synchronised
+        if (pend.empty()) return;
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        for (auto &e : pend) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+                KernelStat &k = g_prof_stats[e.name];
+                k.launches++;
+                k.total_ms += ms;
+                k.alg_bytes += e.bytes;
+            }
+            (void)hipEventDestroy(e.a);
+            (void)hipEventDestroy(e.b);
+        }
+        pend.clear();
     }
     void stage(size_t bytes) {
         if (bytes <= s_host_cap) return;
@@ -325,7 +369,9 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), ctx.G, n, 0},
                           {as<ScD>(const_cast<DBuf &>(cs.aR)), ctx.H, n, 0},
                           {as<ScD>(const_cast<DBuf &>(cs.aO)), ctx.G, n, 1}};
+        int ph = ws.prof_begin("msm_commit", 3.0 * n * (64 + 32));
         pA = ws.msm->enqueue(segA, 3, 2, rowsA);
+        ws.prof_end(ph);
     }
     // s_L, s_R: 2n serial TranscriptRng draws (one Keccak-f each) overlap the MSM
     double t_rng0 = now_ms();
@@ -339,7 +385,9 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         BPG_HIP(hipMemcpyAsync(ws.sL.p, sh, (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, st));
         BPG_HIP(hipMemcpyAsync(ws.sR.p, sh + n, (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, st));
         MsmSeg segS[2] = {{as<ScD>(ws.sL), ctx.G, n, 0}, {as<ScD>(ws.sR), ctx.H, n, 0}};
+        int ph = ws.prof_begin("msm_commit", 2.0 * n * (64 + 32));
         pS = ws.msm->enqueue(segS, 2, 1, rowsS);
+        ws.prof_end(ph);
     }
     BPG_HIP(hipStreamSynchronize(st));
     Point AI, AO, S, tmp;
@@ -386,7 +434,9 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
                as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
                as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
+    int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32 + (double)cs.q * 0 + 36.0 * 1);
     launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
+    ws.prof_end(pfl);
     ScD *wL = as<ScD>(ws.w), *wR = wL + n, *wO = wL + 2 * (size_t)n, *wV = wL + 3 * (size_t)n;
     for (DBuf *d : {&ws.l1, &ws.r0, &ws.r1, &ws.r3}) d->grow((size_t)n * sizeof(ScD) + 64);
     ws.partial.grow(1024 * 8 * sizeof(ScD));
@@ -467,7 +517,9 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         MsmSeg seg[6] = {{ms, Gh + h, h, 0}, {ms + h, Hh, h, 0}, {ms + 4 * (size_t)h, Qdev, 1, 0},
                          {ms + 2 * (size_t)h, Gh, h, 1}, {ms + 3 * (size_t)h, Hh + h, h, 1},
                          {ms + 4 * (size_t)h + 1, Qdev, 1, 1}};
+        int ph = ws.prof_begin("msm_ipp", (4.0 * h + 2) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, 6, 2, rowsLR);
+        ws.prof_end(ph);
         BPG_HIP(hipStreamSynchronize(st));
         Point Lp, Rp;
         combine_rows(Lp, rowsLR, pl.W, pl.c);
@@ -485,7 +537,9 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
             Scalar yh = sc_pow_u64(y_inv, h);
             Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
             PtD *Gn = as<PtD>(ws.Gp[k & 1]), *Hn = as<PtD>(ws.Hp[k & 1]);
+            int pf = ws.prof_begin("ipp_fold_points", 6.0 * h * 64);
             launch_ipp_fold_points(Gh, Hh, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn, st);
+            ws.prof_end(pf);
             Gh = Gn; Hh = Hn;
         }
         lam = lam * uinv;
@@ -496,6 +550,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1011, ws.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
     BPG_HIP(hipStreamSynchronize(st));
     Scalar fa = from_dev(ws.small_host[1010]), fb = from_dev(ws.small_host[1011]);
+    ws.prof_flush();
     double t3 = now_ms();
 
     // R1CSProof::to_bytes (one-phase)

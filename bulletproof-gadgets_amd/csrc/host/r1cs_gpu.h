@@ -68,4 +68,11 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
 
 ProveTimings &last_timings();
 
+// Live kernel instrumentation (bench.py roofline): HIP events around the hot
+// launches on their own stream, resolved after the stream synchronises.
+struct KernelStat { uint64_t launches = 0; double total_ms = 0, alg_bytes = 0; };
+int set_kernel_profiling(bool on);
+bool get_kernel_stat(const char *name, KernelStat &out);
+void reset_kernel_stats();
+
 }  // namespace bpg

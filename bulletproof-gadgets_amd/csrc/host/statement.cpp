@@ -205,6 +205,16 @@ Scalar mimc_hash(const std::vector<uint8_t> &preimage) {
     return state;
 }
 
+Scalar mimc_sponge_native(const std::vector<Scalar> &blocks) {
+    const auto &cs = mimc_consts();
+    Scalar state = Scalar::zero();
+    for (const Scalar &blk : blocks) {
+        state = state + blk;
+        for (const Scalar &c : cs) { Scalar t = state + c; state = t * t * t; }
+    }
+    return state;
+}
+
 // mimc_hash_gadget.rs:108-150
 static LC mimc_sponge(ConstraintSystem &cs, const std::vector<LC> &pre) {
     const auto &consts = mimc_consts();

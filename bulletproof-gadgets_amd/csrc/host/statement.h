@@ -87,6 +87,9 @@ class ConstraintSystem {
 
 // MiMC-256 (src/mimc_hash/mimc.rs:61-75), native.
 Scalar mimc_hash(const std::vector<uint8_t> &preimage);
+// Unpadded sponge over field elements (the Merkle node hash of
+// merkle_tree_gadget.rs:106 evaluated natively).
+Scalar mimc_sponge_native(const std::vector<Scalar> &blocks);
 
 // Statement drivers (src/prove.rs:37-75, src/verify.rs:36-69).
 struct Synthesis {

@@ -193,6 +193,20 @@ const char *bpg_synth_commitments(const bpg_synth *s);
 const uint8_t *bpg_synth_V(const bpg_synth *s);
 void bpg_synth_free(bpg_synth *s);
 
+/* Native MiMC (src/mimc_hash/mimc.rs:61) and the unpadded node sponge
+ * (merkle_tree_gadget.rs:106) for building statements (instances/roots). */
+int bpg_mimc_hash(const uint8_t *data, size_t len, uint8_t out[32]);
+int bpg_mimc_sponge(const uint8_t *blocks, uint32_t count, uint8_t out[32]);
+
+/* Kernel instrumentation: when enabled, launches of the hot kernels are
+ * bracketed by HIP events on their stream; stats accumulate per kernel name
+ * ("ipp_fold_points", "msm_bucket_acc", ...) with the algorithmic HBM bytes
+ * of each launch. */
+int bpg_profile_enable(int on);
+int bpg_kernel_stats(const char *name, uint64_t *launches, double *total_ms,
+                     double *alg_bytes);
+void bpg_kernel_stats_reset(void);
+
 #ifdef __cplusplus
 }
 #endif
