@@ -23,7 +23,8 @@ EXPORTS = [
     "bpg_clear_seed", "bpg_set_device", "bpg_ctx_create", "bpg_ctx_destroy", "bpg_gens_ensure",
     "bpg_pedersen_commit", "bpg_r1cs_prove", "bpg_r1cs_verify", "bpg_prepare", "bpg_prepared_free",
     "bpg_prove_batch", "bpg_last_timings", "bpg_msm", "bpg_synthesize", "bpg_synthesize_verifier",
-    "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free",
+    "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free", "bpg_mimc_hash",
+    "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset",
 ]
 
 

@@ -90,6 +90,9 @@ struct CscDev {
     uint32_t neg_from;         // columns >= neg_from are negated (V and One)
 };
 void launch_flatten(const CscDev &csc, const ScD *zlo, const ScD *zhi, ScD *out, hipStream_t st);
+// one very long column (terms [k0, k1)) by a grid-wide reduction; partial >= 1024 scalars
+void launch_flatten_huge(const CscDev &csc, uint32_t col, uint32_t k0, uint32_t k1, const ScD *zlo, const ScD *zhi,
+                         ScD *partial, ScD *out, hipStream_t st);
 // l(x)/r(x) coefficient vectors (VecPoly3, prover.rs)
 void launch_lr_build(const ScD *aL, const ScD *aR, const ScD *sR, const ScD *wL, const ScD *wR,
                      const ScD *wO, const ScD *yp, const ScD *yip, uint32_t n, ScD *l1, ScD *r0, ScD *r1,

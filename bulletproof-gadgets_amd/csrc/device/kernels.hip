@@ -602,7 +602,7 @@ __global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const 
 }
 // out[k] = R * sum_b partial[b*K + k]   (one block per k)
 __global__ __launch_bounds__(256) void k_reduce_cols(const sc *__restrict__ partial, uint32_t nb, uint32_t K,
-                                                     sc *__restrict__ out, uint32_t out_stride) {
+                                                     sc *__restrict__ out, uint32_t out_stride, int mode) {
     __shared__ sc sh[256];
     uint32_t k = blockIdx.x, tid = threadIdx.x;
     sc acc; sc_zero(acc);
@@ -615,8 +615,12 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const sc *__restrict__ part
     if (tid == 0) {
         sc r, r2;
         sc_load(r, &sh[0]);
-        for (int i = 0; i < 8; i++) r2.v[i] = SC_R2[i];
-        mm(r, r, r2);
+        if (mode == 0) {   // Montgomery-scaled partials: multiply back by R
+            for (int i = 0; i < 8; i++) r2.v[i] = SC_R2[i];
+            mm(r, r, r2);
+        } else if (mode == 2) {
+            sc_neg(r, r);
+        }
         sc_store(out + (size_t)k * out_stride, r);
     }
 }
@@ -625,7 +629,27 @@ void launch_tpoly(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, co
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(n, 256)));
     hipLaunchKernelGGL(k_tpoly, dim3(nb), dim3(256), 0, st, AS_CSC(l1), AS_CSC(l2), AS_CSC(l3), AS_CSC(r0),
                        AS_CSC(r1), AS_CSC(r3), n, AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(6), dim3(256), 0, st, AS_CSC(partial), nb, 6u, AS_SC(out6), 1u);
+    hipLaunchKernelGGL(k_reduce_cols, dim3(6), dim3(256), 0, st, AS_CSC(partial), nb, 6u, AS_SC(out6), 1u, 0);
+    BPG_HIP(hipGetLastError());
+}
+__global__ __launch_bounds__(256) void k_flatten_range(const sc *__restrict__ coeff, const uint32_t *__restrict__ row,
+                                                       uint32_t k0, uint32_t k1, const sc *__restrict__ zlo,
+                                                       const sc *__restrict__ zhi, sc *__restrict__ partial) {
+    sc acc[1];
+    sc_zero(acc[0]);
+    for (uint32_t k = k0 + blockIdx.x * blockDim.x + threadIdx.x; k < k1; k += gridDim.x * blockDim.x) {
+        sc co; sc_load(co, coeff + k);
+        flat_term(acc[0], row[k], co, zlo, zhi);
+    }
+    block_reduce_store<1>(acc, partial);
+}
+void launch_flatten_huge(const CscDev &csc, uint32_t col, uint32_t k0, uint32_t k1, const ScD *zlo, const ScD *zhi,
+                         ScD *partial, ScD *out, hipStream_t st) {
+    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(k1 - k0, 256)));
+    hipLaunchKernelGGL(k_flatten_range, dim3(nb), dim3(256), 0, st, AS_CSC(csc.coeff), csc.row, k0, k1, AS_CSC(zlo),
+                       AS_CSC(zhi), AS_SC(partial));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(256), 0, st, AS_CSC(partial), nb, 1u, AS_SC(out + col), 1u,
+                       col >= csc.neg_from ? 2 : 1);
     BPG_HIP(hipGetLastError());
 }
 __global__ __launch_bounds__(256) void k_dot(const sc *__restrict__ a, const sc *__restrict__ b, uint32_t n,
@@ -642,7 +666,7 @@ __global__ __launch_bounds__(256) void k_dot(const sc *__restrict__ a, const sc 
 void launch_dot(const ScD *a, const ScD *b, uint32_t n, ScD *partial, ScD *out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(n, 256)));
     hipLaunchKernelGGL(k_dot, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), n, AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(256), 0, st, AS_CSC(partial), nb, 1u, AS_SC(out), 1u);
+    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(256), 0, st, AS_CSC(partial), nb, 1u, AS_SC(out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 
@@ -710,7 +734,7 @@ void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundA
                        AS_SC(msm_scal), AS_SC(partial));
     // c_L -> msm_scal[4h], c_R -> msm_scal[4h+1]
     hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
-                       AS_SC(msm_scal + 4 * (size_t)args.h), 1u);
+                       AS_SC(msm_scal + 4 * (size_t)args.h), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 // u, uinv in Montgomery form

@@ -177,7 +177,7 @@ Workspace &thread_workspace(int device) {
     return *p;
 }
 
-ProveTimings &last_timings() { static thread_local ProveTimings t; return t; }
+ProveTimings &last_timings() { static ProveTimings t; return t; }   // last proof on any thread
 
 template <class T>
 static T *as(DBuf &b) { return reinterpret_cast<T *>(b.p); }
@@ -225,8 +225,16 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
             rows[at] = q;
             coef[at] = to_dev(Scalar::reduce(cs->term_coeff + 32 * (size_t)k));
         }
+    // length classes: <= 16 terms -> one thread, <= 4096 -> one wave, larger
+    // (the constant column, some commitments) -> grid-wide reduction
     std::vector<uint32_t> sc_, lc_;
-    for (uint32_t c = 0; c < ncol; c++) ((cnt[c + 1] - cnt[c]) > 16 ? lc_ : sc_).push_back(c);
+    for (uint32_t c = 0; c < ncol; c++) {
+        uint32_t len = cnt[c + 1] - cnt[c];
+        if (P->prover && c == ncol - 1) continue;   // prover never needs wc (Variable::One)
+        if (len > 4096) P->huge_cols.push_back(c);
+        else ((len > 16) ? lc_ : sc_).push_back(c);
+    }
+    P->col_ptr_host = cnt;
     P->nshort = (uint32_t)sc_.size(); P->nlong = (uint32_t)lc_.size();
     auto up = [&](DBuf &d, const void *src, size_t bytes) {
         d.grow(bytes ? bytes : 4);
@@ -436,6 +444,10 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
                as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
     int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32 + (double)cs.q * 0 + 36.0 * 1);
     launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
+    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    for (uint32_t col : cs.huge_cols)
+        launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(ws.zlo), as<ScD>(ws.zhi),
+                            as<ScD>(ws.partial), as<ScD>(ws.w), st);
     ws.prof_end(pfl);
     ScD *wL = as<ScD>(ws.w), *wR = wL + n, *wO = wL + 2 * (size_t)n, *wV = wL + 3 * (size_t)n;
     for (DBuf *d : {&ws.l1, &ws.r0, &ws.r1, &ws.r3}) d->grow((size_t)n * sizeof(ScD) + 64);
@@ -647,6 +659,10 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
                as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
                as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
     launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
+    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    for (uint32_t col : cs.huge_cols)
+        launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(ws.zlo), as<ScD>(ws.zhi),
+                            as<ScD>(ws.partial), as<ScD>(ws.w), st);
     // verification_scalars
     T.append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
     T.append_u64("n", N);

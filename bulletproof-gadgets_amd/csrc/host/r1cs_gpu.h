@@ -43,6 +43,7 @@ struct PreparedCS {
     DBuf aL, aR, aO, vb_dev;            // ScD arrays
     DBuf col_ptr, col_row, col_coeff, short_cols, long_cols;
     uint32_t nshort = 0, nlong = 0, ncol = 0;
+    std::vector<uint32_t> huge_cols, col_ptr_host;
     ~PreparedCS();
 };
 
