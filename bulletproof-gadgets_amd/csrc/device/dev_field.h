@@ -3,12 +3,13 @@
 // Replaces the curve25519-dalek 3.2.0 serial/u64 + avx2 backends (field.rs,
 // scalar.rs, ristretto.rs, edwards.rs) for the device side of the hot path.
 // Representation is chosen for CDNA4's VALU, not translated from dalek:
-//   * field elements: 8 x 32-bit limbs, radix 2^32, any value < 2^256 that is
-//     congruent mod p ("weakly reduced"); products use v_mad_u64_u32 chains and
-//     fold with 2^256 == 38 (mod p). Canonical form only at encode/compare.
+//   * field elements: 10 limbs of 26/25 bits (radix 2^25.5), carry-free
+//     64-bit column sums (v_mad_u64_u32), 2^255 == 19 folding; canonical
+//     form only at encode/compare (details and bounds below).
 //   * scalars: 8 x 32-bit limbs, canonical (< l); products by 32-bit CIOS
 //     Montgomery (R = 2^256), no MFMA — this is 255-bit integer work.
-//   * points: extended twisted-Edwards (X:Y:Z:T), a = -1, 128 bytes.
+//   * points: extended twisted-Edwards (X:Y:Z:T), a = -1, 160 bytes; cached
+//     (Y+X, Y-X, 2Z, 2dT) right operands for 8M additions.
 #pragma once
 #include <stdint.h>
 #ifdef BPG_HOST_SIM
@@ -24,15 +25,49 @@ static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
 #define DEVI __device__ __forceinline__
 #endif
 
-struct fe { uint32_t v[8]; };
+// Field elements: 10 limbs, radix 2^25.5 (widths 26,25,26,...; limb i sits
+// at bit ceil(25.5 i)). Measured on gfx950 (csrc/bench/fe_variants.hip):
+// v_mad_u64_u32 issues at full rate, and 100 carry-free 64-bit
+// multiply-accumulates into column sums plus one carry pass beat an 8x32-bit
+// schoolbook product by 1.6x (the 32-bit carry chains cost more in moves
+// and 64-bit adds than the extra multiplies).
+//
+// Bounds. "T" (tight) = each limb <= mask + 2^17; every fe_mul / fe_sq /
+// fe_carry output and every stored coordinate is T. Unreduced sums are
+// allowed where the bound is tracked (tests/test_devsim.py checks the worst
+// cases):
+//   fe_add_nc(T,T) <= 2T;  fe_sub_nc(a, T) <= a + 2T;  fe_sub4_nc(a, <=3T) <= a + 4T
+//   fe_mul(f, g): f <= 5T (6T if g <= 2T), g <= 3T   (column sums < 2^64,
+//   19 g_j < 2^32);  fe_sq(f): f <= 3T.
+// fe_add / fe_sub / fe_neg (no suffix) carry and return T.
+struct fe { uint32_t v[10]; };
 struct sc { uint32_t v[8]; };
-struct ge { fe X, Y, Z, T; };
+struct ge { fe X, Y, Z, T; };           // extended twisted Edwards, a = -1
+struct gec { fe YpX, YmX, Z2, T2d; };   // cached: (Y+X, Y-X, 2Z, 2dT)
+
+#define FE_M26 0x3ffffffu
+#define FE_M25 0x1ffffffu
+DEVI constexpr int fe_width(int i) { return (i & 1) ? 25 : 26; }
+DEVI constexpr int fe_pos(int i) { return (i >> 1) * 51 + ((i & 1) ? 26 : 0); }
+
+// 8 little-endian 32-bit words (bit 255 ignored) -> limbs
+DEVI constexpr fe fe_from_words(const uint32_t w0, const uint32_t w1, const uint32_t w2, const uint32_t w3,
+                                const uint32_t w4, const uint32_t w5, const uint32_t w6, const uint32_t w7) {
+    fe r{};
+    const uint32_t w[9] = {w0, w1, w2, w3, w4, w5, w6, w7, 0};
+    for (int i = 0; i < 10; i++) {
+        int p = fe_pos(i), wi = p >> 5, sh = p & 31;
+        uint64_t x = ((uint64_t)w[wi] | ((uint64_t)w[wi + 1] << 32)) >> sh;
+        r.v[i] = (uint32_t)x & ((1u << fe_width(i)) - 1);
+    }
+    return r;
+}
 
 // ---------------------------------------------------------------------------
 // constants (derivation: oracle/gen_consts.py; values per RFC 9496 §4.1)
 // ---------------------------------------------------------------------------
 #define FE_C(name, a0, a1, a2, a3, a4, a5, a6, a7) \
-    static __device__ __constant__ const fe name = {{a0, a1, a2, a3, a4, a5, a6, a7}};
+    static __device__ __constant__ const fe name = fe_from_words(a0, a1, a2, a3, a4, a5, a6, a7);
 FE_C(FE_D, 0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du, 0x7779e898u, 0x8cc74079u, 0x2b6ffe73u, 0x52036ceeu)
 FE_C(FE_D2, 0x26b2f159u, 0xebd69b94u, 0x8283b156u, 0x00e0149au, 0xeef3d130u, 0x198e80f2u, 0x56dffce7u, 0x2406d9dcu)
 FE_C(FE_SQRT_M1, 0x4a0ea0b0u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u, 0x3dfbd7a7u, 0x2b4d0099u, 0x4fc1df0bu, 0x2b832480u)
@@ -51,85 +86,122 @@ static __device__ __constant__ const uint32_t SC_R2[8] = {0x449c0f01u, 0xa40611e
 // ---------------------------------------------------------------------------
 DEVI void fe_zero(fe &r) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = 0;
+    for (int i = 0; i < 10; i++) r.v[i] = 0;
 }
 DEVI void fe_one(fe &r) { fe_zero(r); r.v[0] = 1; }
 
-DEVI void fe_add(fe &r, const fe &a, const fe &b) {
-    uint64_t c = 0;
+// weak reduction to T: every limb to its width plus the incoming carry
+DEVI void fe_carry(fe &r, const fe &a) {
+    uint32_t c[10];
 #pragma unroll
-    for (int i = 0; i < 8; i++) { c += (uint64_t)a.v[i] + b.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    c *= 38;
+    for (int i = 0; i < 10; i++) c[i] = a.v[i] >> fe_width(i);
+    r.v[0] = (a.v[0] & FE_M26) + 19 * c[9];
 #pragma unroll
-    for (int i = 0; i < 8; i++) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    r.v[0] += (uint32_t)c * 38;
+    for (int i = 1; i < 10; i++) r.v[i] = (a.v[i] & ((i & 1) ? FE_M25 : FE_M26)) + c[i - 1];
 }
-
-DEVI void fe_sub(fe &r, const fe &a, const fe &b) {
-    int64_t c = 0;
+DEVI void fe_add_nc(fe &r, const fe &a, const fe &b) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) { c += (int64_t)a.v[i] - (int64_t)b.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    // c in {-1, 0}: a wrap by 2^256 == +38, take it back
-    c *= 38;
-#pragma unroll
-    for (int i = 0; i < 8; i++) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    r.v[0] += (uint32_t)((int32_t)c * 38);
+    for (int i = 0; i < 10; i++) r.v[i] = a.v[i] + b.v[i];
 }
-
+// a - b + 2p (b <= T)
+DEVI void fe_sub_nc(fe &r, const fe &a, const fe &b) {
+    r.v[0] = a.v[0] + 0x7ffffdau - b.v[0];
+#pragma unroll
+    for (int i = 1; i < 10; i++) r.v[i] = a.v[i] + ((i & 1) ? 0x3fffffeu : 0x7fffffeu) - b.v[i];
+}
+// a - b + 4p (b <= 3T)
+DEVI void fe_sub4_nc(fe &r, const fe &a, const fe &b) {
+    r.v[0] = a.v[0] + 0xfffffb4u - b.v[0];
+#pragma unroll
+    for (int i = 1; i < 10; i++) r.v[i] = a.v[i] + ((i & 1) ? 0x7fffffcu : 0xffffffcu) - b.v[i];
+}
+DEVI void fe_add(fe &r, const fe &a, const fe &b) { fe t; fe_add_nc(t, a, b); fe_carry(r, t); }
+DEVI void fe_sub(fe &r, const fe &a, const fe &b) { fe t; fe_sub4_nc(t, a, b); fe_carry(r, t); }
 DEVI void fe_neg(fe &r, const fe &a) { fe z; fe_zero(z); fe_sub(r, z, a); }
 
-// 16-limb product -> fold with 38
-DEVI void fe_reduce16(fe &r, const uint32_t t[16]) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) { c += (uint64_t)t[8 + i] * 38u + t[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    c *= 38;
-#pragma unroll
-    for (int i = 0; i < 8; i++) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    r.v[0] += (uint32_t)c * 38;
+DEVI uint64_t fe_m64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+
+// column sums -> T (carry order keeps every intermediate < 2^64)
+DEVI void fe_carry_cols(fe &r, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3, uint64_t h4, uint64_t h5,
+                        uint64_t h6, uint64_t h7, uint64_t h8, uint64_t h9) {
+    uint64_t c;
+    c = h0 >> 26; h1 += c; h0 &= FE_M26;
+    c = h4 >> 26; h5 += c; h4 &= FE_M26;
+    c = h1 >> 25; h2 += c; h1 &= FE_M25;
+    c = h5 >> 25; h6 += c; h5 &= FE_M25;
+    c = h2 >> 26; h3 += c; h2 &= FE_M26;
+    c = h6 >> 26; h7 += c; h6 &= FE_M26;
+    c = h3 >> 25; h4 += c; h3 &= FE_M25;
+    c = h7 >> 25; h8 += c; h7 &= FE_M25;
+    c = h4 >> 26; h5 += c; h4 &= FE_M26;
+    c = h8 >> 26; h9 += c; h8 &= FE_M26;
+    c = h9 >> 25; h0 += c * 19; h9 &= FE_M25;
+    c = h0 >> 26; h1 += c; h0 &= FE_M26;
+    r.v[0] = (uint32_t)h0; r.v[1] = (uint32_t)h1; r.v[2] = (uint32_t)h2; r.v[3] = (uint32_t)h3;
+    r.v[4] = (uint32_t)h4; r.v[5] = (uint32_t)h5; r.v[6] = (uint32_t)h6; r.v[7] = (uint32_t)h7;
+    r.v[8] = (uint32_t)h8; r.v[9] = (uint32_t)h9;
 }
 
-DEVI void fe_mul(fe &r, const fe &a, const fe &b) {
-    uint32_t t[16];
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) { c += (uint64_t)a.v[0] * b.v[j]; t[j] = (uint32_t)c; c >>= 32; }
-    t[8] = (uint32_t)c;
-#pragma unroll
-    for (int i = 1; i < 8; i++) {
-        c = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) { c += (uint64_t)a.v[i] * b.v[j] + t[i + j]; t[i + j] = (uint32_t)c; c >>= 32; }
-        t[i + 8] = (uint32_t)c;
-    }
-    fe_reduce16(r, t);
+DEVI void fe_mul(fe &h, const fe &f, const fe &g) {
+    const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4], f5 = f.v[5], f6 = f.v[6],
+                   f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+    const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4], g5 = g.v[5], g6 = g.v[6],
+                   g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
+    const uint32_t g1_19 = 19 * g1, g2_19 = 19 * g2, g3_19 = 19 * g3, g4_19 = 19 * g4, g5_19 = 19 * g5,
+                   g6_19 = 19 * g6, g7_19 = 19 * g7, g8_19 = 19 * g8, g9_19 = 19 * g9;
+    const uint32_t f1_2 = 2 * f1, f3_2 = 2 * f3, f5_2 = 2 * f5, f7_2 = 2 * f7, f9_2 = 2 * f9;
+    uint64_t h0 = fe_m64(f0, g0) + fe_m64(f1_2, g9_19) + fe_m64(f2, g8_19) + fe_m64(f3_2, g7_19) +
+                  fe_m64(f4, g6_19) + fe_m64(f5_2, g5_19) + fe_m64(f6, g4_19) + fe_m64(f7_2, g3_19) +
+                  fe_m64(f8, g2_19) + fe_m64(f9_2, g1_19);
+    uint64_t h1 = fe_m64(f0, g1) + fe_m64(f1, g0) + fe_m64(f2, g9_19) + fe_m64(f3, g8_19) + fe_m64(f4, g7_19) +
+                  fe_m64(f5, g6_19) + fe_m64(f6, g5_19) + fe_m64(f7, g4_19) + fe_m64(f8, g3_19) + fe_m64(f9, g2_19);
+    uint64_t h2 = fe_m64(f0, g2) + fe_m64(f1_2, g1) + fe_m64(f2, g0) + fe_m64(f3_2, g9_19) + fe_m64(f4, g8_19) +
+                  fe_m64(f5_2, g7_19) + fe_m64(f6, g6_19) + fe_m64(f7_2, g5_19) + fe_m64(f8, g4_19) +
+                  fe_m64(f9_2, g3_19);
+    uint64_t h3 = fe_m64(f0, g3) + fe_m64(f1, g2) + fe_m64(f2, g1) + fe_m64(f3, g0) + fe_m64(f4, g9_19) +
+                  fe_m64(f5, g8_19) + fe_m64(f6, g7_19) + fe_m64(f7, g6_19) + fe_m64(f8, g5_19) + fe_m64(f9, g4_19);
+    uint64_t h4 = fe_m64(f0, g4) + fe_m64(f1_2, g3) + fe_m64(f2, g2) + fe_m64(f3_2, g1) + fe_m64(f4, g0) +
+                  fe_m64(f5_2, g9_19) + fe_m64(f6, g8_19) + fe_m64(f7_2, g7_19) + fe_m64(f8, g6_19) +
+                  fe_m64(f9_2, g5_19);
+    uint64_t h5 = fe_m64(f0, g5) + fe_m64(f1, g4) + fe_m64(f2, g3) + fe_m64(f3, g2) + fe_m64(f4, g1) +
+                  fe_m64(f5, g0) + fe_m64(f6, g9_19) + fe_m64(f7, g8_19) + fe_m64(f8, g7_19) + fe_m64(f9, g6_19);
+    uint64_t h6 = fe_m64(f0, g6) + fe_m64(f1_2, g5) + fe_m64(f2, g4) + fe_m64(f3_2, g3) + fe_m64(f4, g2) +
+                  fe_m64(f5_2, g1) + fe_m64(f6, g0) + fe_m64(f7_2, g9_19) + fe_m64(f8, g8_19) + fe_m64(f9_2, g7_19);
+    uint64_t h7 = fe_m64(f0, g7) + fe_m64(f1, g6) + fe_m64(f2, g5) + fe_m64(f3, g4) + fe_m64(f4, g3) +
+                  fe_m64(f5, g2) + fe_m64(f6, g1) + fe_m64(f7, g0) + fe_m64(f8, g9_19) + fe_m64(f9, g8_19);
+    uint64_t h8 = fe_m64(f0, g8) + fe_m64(f1_2, g7) + fe_m64(f2, g6) + fe_m64(f3_2, g5) + fe_m64(f4, g4) +
+                  fe_m64(f5_2, g3) + fe_m64(f6, g2) + fe_m64(f7_2, g1) + fe_m64(f8, g0) + fe_m64(f9_2, g9_19);
+    uint64_t h9 = fe_m64(f0, g9) + fe_m64(f1, g8) + fe_m64(f2, g7) + fe_m64(f3, g6) + fe_m64(f4, g5) +
+                  fe_m64(f5, g4) + fe_m64(f6, g3) + fe_m64(f7, g2) + fe_m64(f8, g1) + fe_m64(f9, g0);
+    fe_carry_cols(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
 }
 
-DEVI void fe_sq(fe &r, const fe &a) {
-    uint32_t t[16];
-    // off-diagonal products a_i a_j (i < j)
-#pragma unroll
-    for (int i = 0; i < 16; i++) t[i] = 0;
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-        uint64_t c = 0;
-#pragma unroll
-        for (int j = i + 1; j < 8; j++) { c += (uint64_t)a.v[i] * a.v[j] + t[i + j]; t[i + j] = (uint32_t)c; c >>= 32; }
-        t[i + 8] = (uint32_t)c;
-    }
-    // double
-    uint32_t hi = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) { uint32_t x = t[i]; t[i] = (x << 1) | hi; hi = x >> 31; }
-    // add squares
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        uint64_t s = (uint64_t)a.v[i] * a.v[i];
-        c += (uint64_t)t[2 * i] + (uint32_t)s; t[2 * i] = (uint32_t)c; c >>= 32;
-        c += (uint64_t)t[2 * i + 1] + (uint32_t)(s >> 32); t[2 * i + 1] = (uint32_t)c; c >>= 32;
-    }
-    fe_reduce16(r, t);
+// 55 products (symmetric terms doubled up front)
+DEVI void fe_sq(fe &h, const fe &f) {
+    const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4], f5 = f.v[5], f6 = f.v[6],
+                   f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+    const uint32_t f0_2 = 2 * f0, f1_2 = 2 * f1, f2_2 = 2 * f2, f3_2 = 2 * f3, f4_2 = 2 * f4, f5_2 = 2 * f5,
+                   f6_2 = 2 * f6, f7_2 = 2 * f7;
+    const uint32_t f5_38 = 38 * f5, f6_19 = 19 * f6, f7_38 = 38 * f7, f8_19 = 19 * f8, f9_38 = 38 * f9;
+    uint64_t h0 = fe_m64(f0, f0) + fe_m64(f1_2, f9_38) + fe_m64(f2_2, f8_19) + fe_m64(f3_2, f7_38) +
+                  fe_m64(f4_2, f6_19) + fe_m64(f5, f5_38);
+    uint64_t h1 = fe_m64(f0_2, f1) + fe_m64(f2, f9_38) + fe_m64(f3_2, f8_19) + fe_m64(f4, f7_38) +
+                  fe_m64(f5_2, f6_19);
+    uint64_t h2 = fe_m64(f0_2, f2) + fe_m64(f1_2, f1) + fe_m64(f3_2, f9_38) + fe_m64(f4_2, f8_19) +
+                  fe_m64(f5_2, f7_38) + fe_m64(f6, f6_19);
+    uint64_t h3 = fe_m64(f0_2, f3) + fe_m64(f1_2, f2) + fe_m64(f4, f9_38) + fe_m64(f5_2, f8_19) +
+                  fe_m64(f6, f7_38);
+    uint64_t h4 = fe_m64(f0_2, f4) + fe_m64(f1_2, f3_2) + fe_m64(f2, f2) + fe_m64(f5_2, f9_38) +
+                  fe_m64(f6_2, f8_19) + fe_m64(f7, f7_38);
+    uint64_t h5 = fe_m64(f0_2, f5) + fe_m64(f1_2, f4) + fe_m64(f2_2, f3) + fe_m64(f6, f9_38) +
+                  fe_m64(f7_2, f8_19);
+    uint64_t h6 = fe_m64(f0_2, f6) + fe_m64(f1_2, f5_2) + fe_m64(f2_2, f4) + fe_m64(f3_2, f3) +
+                  fe_m64(f7_2, f9_38) + fe_m64(f8, f8_19);
+    uint64_t h7 = fe_m64(f0_2, f7) + fe_m64(f1_2, f6) + fe_m64(f2_2, f5) + fe_m64(f3_2, f4) + fe_m64(f8, f9_38);
+    uint64_t h8 = fe_m64(f0_2, f8) + fe_m64(f1_2, f7_2) + fe_m64(f2_2, f6) + fe_m64(f3_2, f5_2) +
+                  fe_m64(f4, f4) + fe_m64(f9, f9_38);
+    uint64_t h9 = fe_m64(f0_2, f9) + fe_m64(f1_2, f8) + fe_m64(f2_2, f7) + fe_m64(f3_2, f6) + fe_m64(f4_2, f5);
+    fe_carry_cols(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
 }
 
 DEVI void fe_sqn(fe &r, const fe &a, int n) {
@@ -137,46 +209,57 @@ DEVI void fe_sqn(fe &r, const fe &a, int n) {
     for (int i = 1; i < n; i++) fe_sq(r, r);
 }
 
-// Fully reduce to [0, p).
+// Fully reduce to the canonical representative in [0, p), limbs at width.
 DEVI void fe_canon(fe &r, const fe &a) {
-    r = a;
-    // fold bit 255 (2^255 == 19): r < 2^255 + 19
-    uint64_t c = (uint64_t)(r.v[7] >> 31) * 19;
-    r.v[7] &= 0x7fffffffu;
+    uint32_t h[10];
 #pragma unroll
-    for (int i = 0; i < 8; i++) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
-    // r >= p  <=>  t = r + 19 has bit 255 set; then r - p = t - 2^255
-    uint32_t t[8];
-    c = 19;
+    for (int i = 0; i < 10; i++) h[i] = a.v[i];
+    // two sequential carry passes: value < 2^255 + small, limbs at width
 #pragma unroll
-    for (int i = 0; i < 8; i++) { c += r.v[i]; t[i] = (uint32_t)c; c >>= 32; }
-    if (t[7] >> 31) {
-        t[7] &= 0x7fffffffu;
+    for (int pass = 0; pass < 2; pass++) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) r.v[i] = t[i];
+        for (int i = 0; i < 9; i++) { h[i + 1] += h[i] >> fe_width(i); h[i] &= (i & 1) ? FE_M25 : FE_M26; }
+        h[0] += 19 * (h[9] >> 25); h[9] &= FE_M25;
     }
+    // h >= p  <=>  h + 19 >= 2^255
+    uint32_t q = (h[0] + 19) >> 26;
+#pragma unroll
+    for (int i = 1; i < 10; i++) q = (h[i] + q) >> fe_width(i);
+    h[0] += 19 * q;
+#pragma unroll
+    for (int i = 0; i < 9; i++) { h[i + 1] += h[i] >> fe_width(i); h[i] &= (i & 1) ? FE_M25 : FE_M26; }
+    h[9] &= FE_M25;
+#pragma unroll
+    for (int i = 0; i < 10; i++) r.v[i] = h[i];
 }
 
-DEVI void fe_tobytes(uint8_t s[32], const fe &a) {
+// canonical 8 x 32-bit words
+DEVI void fe_tow(uint32_t w[8], const fe &a) {
     fe c; fe_canon(c, a);
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        s[4 * i] = (uint8_t)c.v[i]; s[4 * i + 1] = (uint8_t)(c.v[i] >> 8);
-        s[4 * i + 2] = (uint8_t)(c.v[i] >> 16); s[4 * i + 3] = (uint8_t)(c.v[i] >> 24);
+    for (int i = 0; i < 8; i++) w[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const int p = fe_pos(i), wi = p >> 5, sh = p & 31;
+        w[wi] |= c.v[i] << sh;
+        if (sh + fe_width(i) > 32 && wi + 1 < 8) w[wi + 1] |= c.v[i] >> (32 - sh);
     }
 }
-DEVI void fe_tow(uint32_t w[8], const fe &a) { fe c; fe_canon(c, a); for (int i = 0; i < 8; i++) w[i] = c.v[i]; }
-// FieldElement::from_bytes: bit 255 ignored.
-DEVI void fe_fromw(fe &r, const uint32_t w[8]) {
+DEVI void fe_tobytes(uint8_t s[32], const fe &a) {
+    uint32_t w[8]; fe_tow(w, a);
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = w[i];
-    r.v[7] &= 0x7fffffffu;
+    for (int i = 0; i < 8; i++) {
+        s[4 * i] = (uint8_t)w[i]; s[4 * i + 1] = (uint8_t)(w[i] >> 8);
+        s[4 * i + 2] = (uint8_t)(w[i] >> 16); s[4 * i + 3] = (uint8_t)(w[i] >> 24);
+    }
 }
+// FieldElement::from_bytes: bit 255 ignored.
+DEVI void fe_fromw(fe &r, const uint32_t w[8]) { r = fe_from_words(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]); }
 DEVI bool fe_iszero(const fe &a) {
     fe c; fe_canon(c, a);
     uint32_t acc = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) acc |= c.v[i];
+    for (int i = 0; i < 10; i++) acc |= c.v[i];
     return acc == 0;
 }
 DEVI bool fe_isneg(const fe &a) { fe c; fe_canon(c, a); return c.v[0] & 1; }
@@ -332,30 +415,78 @@ DEVI bool sc_iszero(const sc &a) {
 }
 
 // ---------------------------------------------------------------------------
-// Edwards points, extended coordinates
+// Edwards points. Extended (X:Y:Z:T), T = XY/Z; cached (Y+X, Y-X, 2Z, 2dT)
+// for the right operand of additions. All coordinates T on output.
 // ---------------------------------------------------------------------------
 DEVI void ge_identity(ge &p) { fe_zero(p.X); fe_one(p.Y); fe_one(p.Z); fe_zero(p.T); }
-// add-2008-hwcd-3, a = -1
+DEVI void gec_identity(gec &c) { fe_one(c.YpX); fe_one(c.YmX); fe_zero(c.Z2); c.Z2.v[0] = 2; fe_zero(c.T2d); }
+DEVI void ge_to_cached(gec &c, const ge &p) {
+    fe_add(c.YpX, p.Y, p.X);
+    fe_sub(c.YmX, p.Y, p.X);
+    fe_add(c.Z2, p.Z, p.Z);
+    fe_mul(c.T2d, p.T, FE_D2);
+}
+// -c: swap Y+X / Y-X and negate 2dT
+DEVI void gec_neg(gec &r, const gec &c) { r.YpX = c.YmX; r.YmX = c.YpX; r.Z2 = c.Z2; fe_neg(r.T2d, c.T2d); }
+DEVI void gec_cneg(gec &c, bool neg) {
+    if (neg) { fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; fe_neg(c.T2d, c.T2d); }
+}
+// add-2008-hwcd-3 (a = -1) with a cached right operand: 8M
+DEVI void ge_add_c(ge &r, const ge &p, const gec &q) {
+    fe a, b, c, d, e, f, g, h;
+    fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q.YmX);       // 3T x T
+    fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q.YpX);       // 2T x T
+    fe_mul(c, p.T, q.T2d);
+    fe_mul(d, p.Z, q.Z2);
+    fe_sub_nc(e, b, a);                                 // 3T
+    fe_sub_nc(f, d, c);                                 // 3T
+    fe_add_nc(g, d, c);                                 // 2T
+    fe_add_nc(h, b, a);                                 // 2T
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+}
+DEVI void ge_sub_c(ge &r, const ge &p, const gec &q) {
+    fe a, b, c, d, e, f, g, h;
+    fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q.YpX);
+    fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q.YmX);
+    fe_mul(c, p.T, q.T2d);
+    fe_mul(d, p.Z, q.Z2);
+    fe_sub_nc(e, b, a);
+    fe_add_nc(f, d, c);                                 // D + C for -q
+    fe_sub_nc(g, d, c);
+    fe_add_nc(h, b, a);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
+}
+// extended + extended (cached form of q built on the fly, unreduced): 9M
 DEVI void ge_add(ge &r, const ge &p, const ge &q) {
     fe a, b, c, d, e, f, g, h, t;
-    fe_sub(a, p.Y, p.X); fe_sub(t, q.Y, q.X); fe_mul(a, a, t);
-    fe_add(b, p.Y, p.X); fe_add(t, q.Y, q.X); fe_mul(b, b, t);
+    fe_sub_nc(a, p.Y, p.X); fe_sub_nc(t, q.Y, q.X); fe_mul(a, a, t);   // 3T x 3T
+    fe_add_nc(b, p.Y, p.X); fe_add_nc(t, q.Y, q.X); fe_mul(b, b, t);   // 2T x 2T
     fe_mul(c, p.T, q.T); fe_mul(c, c, FE_D2);
-    fe_mul(d, p.Z, q.Z); fe_add(d, d, d);
-    fe_sub(e, b, a); fe_sub(f, d, c); fe_add(g, d, c); fe_add(h, b, a);
+    fe_add_nc(t, q.Z, q.Z); fe_mul(d, p.Z, t);                         // T x 2T
+    fe_sub_nc(e, b, a);
+    fe_sub_nc(f, d, c);
+    fe_add_nc(g, d, c);
+    fe_add_nc(h, b, a);
     fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
 }
 DEVI void ge_neg(ge &r, const ge &p) { fe_neg(r.X, p.X); r.Y = p.Y; r.Z = p.Z; fe_neg(r.T, p.T); }
 DEVI void ge_sub(ge &r, const ge &p, const ge &q) { ge n; ge_neg(n, q); ge_add(r, p, n); }
-// dbl-2008-hwcd (a = -1), 4M + 4S
-DEVI void ge_dbl(ge &r, const ge &p) {
+// dbl-2008-hwcd (a = -1): 4M + 4S; with_t = false skips T (3M + 4S), for
+// doublings followed by another doubling (T is not an input of doubling).
+template <bool with_t>
+DEVI void ge_dbl_t(ge &r, const ge &p) {
     fe xx, yy, zz2, xpy2, ypx, ymx, ex, tc;
-    fe_sq(xx, p.X); fe_sq(yy, p.Y); fe_sq(zz2, p.Z); fe_add(zz2, zz2, zz2);
-    fe_add(xpy2, p.X, p.Y); fe_sq(xpy2, xpy2);
-    fe_add(ypx, yy, xx); fe_sub(ymx, yy, xx);
-    fe_sub(ex, xpy2, ypx); fe_sub(tc, zz2, ymx);
-    fe_mul(r.X, ex, tc); fe_mul(r.Y, ypx, ymx); fe_mul(r.Z, ymx, tc); fe_mul(r.T, ex, ypx);
+    fe_sq(xx, p.X); fe_sq(yy, p.Y); fe_sq(zz2, p.Z);
+    fe_add_nc(zz2, zz2, zz2);                           // 2T
+    fe_add_nc(xpy2, p.X, p.Y); fe_sq(xpy2, xpy2);       // sq(2T)
+    fe_add_nc(ypx, yy, xx);                             // 2T
+    fe_sub_nc(ymx, yy, xx);                             // 3T
+    fe_sub4_nc(ex, xpy2, ypx);                          // 5T
+    fe_sub4_nc(tc, zz2, ymx); fe_carry(tc, tc);         // 6T -> T
+    fe_mul(r.X, ex, tc); fe_mul(r.Y, ypx, ymx); fe_mul(r.Z, ymx, tc);
+    if (with_t) fe_mul(r.T, ex, ypx);
 }
+DEVI void ge_dbl(ge &r, const ge &p) { ge_dbl_t<true>(r, p); }
 DEVI bool ge_is_identity(const ge &p) { return fe_iszero(p.X) || fe_iszero(p.Y); }
 
 // RistrettoPoint::compress -> 8 canonical words
@@ -431,23 +562,28 @@ DEVI void ristretto_elligator(ge &p, const fe &r0) {
 }
 
 // ---------------------------------------------------------------------------
-// memory helpers: points are 128 B (X,Y,Z,T), loaded as 8 x uint4
+// memory helpers: points are 160 B (X,Y,Z,T as 10 limbs), moved as 10 x uint4
 // ---------------------------------------------------------------------------
-DEVI void ge_load(ge &p, const ge *src) {
+template <class P>
+DEVI void pt_load(P &p, const P *src) {
+    static_assert(sizeof(P) == 160, "point layout");
     const uint4 *s = reinterpret_cast<const uint4 *>(src);
-    uint4 q[8];
+    uint4 q[10];
 #pragma unroll
-    for (int i = 0; i < 8; i++) q[i] = s[i];
+    for (int i = 0; i < 10; i++) q[i] = s[i];
     uint32_t *d = reinterpret_cast<uint32_t *>(&p);
 #pragma unroll
-    for (int i = 0; i < 8; i++) { d[4 * i] = q[i].x; d[4 * i + 1] = q[i].y; d[4 * i + 2] = q[i].z; d[4 * i + 3] = q[i].w; }
+    for (int i = 0; i < 10; i++) { d[4 * i] = q[i].x; d[4 * i + 1] = q[i].y; d[4 * i + 2] = q[i].z; d[4 * i + 3] = q[i].w; }
 }
-DEVI void ge_store(ge *dst, const ge &p) {
+template <class P>
+DEVI void pt_store(P *dst, const P &p) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
     const uint32_t *s = reinterpret_cast<const uint32_t *>(&p);
 #pragma unroll
-    for (int i = 0; i < 8; i++) d[i] = make_uint4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
+    for (int i = 0; i < 10; i++) d[i] = make_uint4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
 }
+DEVI void ge_load(ge &p, const ge *src) { pt_load(p, src); }
+DEVI void ge_store(ge *dst, const ge &p) { pt_store(dst, p); }
 DEVI void sc_load(sc &r, const sc *src) {
     const uint4 *s = reinterpret_cast<const uint4 *>(src);
     uint4 a = s[0], b = s[1];

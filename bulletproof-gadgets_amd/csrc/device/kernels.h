@@ -9,10 +9,10 @@
 namespace bpg {
 namespace dev {
 
-// Device layouts (must match dev_field.h): 32 B scalars / field elements,
-// 128 B extended points (X, Y, Z, T).
+// Device layouts (must match dev_field.h): 32 B scalars, 160 B extended
+// points (X, Y, Z, T; each 10 limbs of 26/25 bits).
 struct ScD { uint32_t v[8]; };
-struct PtD { uint32_t v[32]; };
+struct PtD { uint32_t v[40]; };
 
 #define BPG_HIP(x)                                                                 \
     do {                                                                           \
@@ -119,8 +119,12 @@ void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundA
                      ScD *partial, hipStream_t st);
 void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st);
 // Ghat' = Ghat_L + rho * Ghat_R (rho = rho_a except lanes i < n <= h+i, which use rho_b)
+// Kernel-argument block staged through pinned host memory to a device buffer
+// (one per stream; the host side is rewritten only after the stream has
+// passed the previous use).
+struct ArgStage { void *dev = nullptr, *host = nullptr; };
 void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
-                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, hipStream_t st);
+                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage, hipStream_t st);
 // verifier helpers
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
                       ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st);

@@ -347,10 +347,10 @@ void MsmEngine::reserve(const MsmPlan &p) {
     cnt_.grow(nch * 4); off_.grow(nch * 4);
     E_.grow(64 * 4);
     rk_a_.grow(p.capE * 4); rk_b_.grow(p.capE * 4);
-    rp_a_.grow(p.capE * 128); rp_b_.grow(p.capE * 128);
-    buckets_.grow((size_t)p.rows * p.half * 128);
-    segacc_.grow((size_t)p.rows * p.nseg_per_row * 128);
-    rows_dev_.grow((size_t)p.rows * 128);
+    rp_a_.grow(p.capE * sizeof(ge)); rp_b_.grow(p.capE * sizeof(ge));
+    buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
+    segacc_.grow((size_t)p.rows * p.nseg_per_row * sizeof(ge));
+    rows_dev_.grow((size_t)p.rows * sizeof(ge));
 }
 
 MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host) {
@@ -389,7 +389,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         for (int r = 0; r < p.rows; r++) {
             ge id;
             uint32_t *w = reinterpret_cast<uint32_t *>(&rows_host[r]);
-            memset(w, 0, 128); w[8] = 1; w[16] = 1;
+            memset(w, 0, sizeof(PtD)); w[10] = 1; w[20] = 1;
             (void)id;
         }
         return p;
@@ -446,7 +446,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, AS_CGE(segacc_.p), (uint32_t)p.nseg_per_row,
                        AS_GE(rows_dev_.p));
     BPG_HIP(hipGetLastError());
-    BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * 128, hipMemcpyDeviceToHost, st_));
+    BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;
 }
 
@@ -750,77 +750,152 @@ void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStr
                        *reinterpret_cast<sc *>(&u), *reinterpret_cast<sc *>(&uinv));
     BPG_HIP(hipGetLastError());
 }
-// NAF double-and-add of a (per-lane selected) scalar, then + P_L
-DEVI void naf_mul_add(ge &out, const ge &PL, const ge &PR, const sc &k0) {
-    // NAF digits LSB-first into pos/neg bitmasks (<= 254 digits for k < 2^253)
-    uint32_t pos[9], neg[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) { pos[i] = 0; neg[i] = 0; }
-    uint32_t k[9];
-#pragma unroll
-    for (int i = 0; i < 8; i++) k[i] = k0.v[i];
-    k[8] = 0;
-    int top = -1;
-    for (int bit = 0; bit < 260; bit++) {
-        bool any = false;
-#pragma unroll
-        for (int i = 0; i < 9; i++) any = any || k[i];
-        if (!any) break;
-        if (k[0] & 1) {
-            uint32_t r = k[0] & 3;
-            if (r == 1) {
-                pos[bit >> 5] |= 1u << (bit & 31);
-                k[0] &= ~1u;
+// Point fold: out_i = P_L,i + rho * P_R,i with one rho per lane class. rho is
+// uniform across a block, so its width-4 wNAF schedule (digits in +-{1,3,5,7},
+// top digit first, with the doubling count before each digit) is computed on
+// the host and read from kernel arguments (scalar loads, no divergence). The
+// odd multiples P, 3P, 5P, 7P of each lane's P_R live in registers as cached
+// points; doublings that feed another doubling skip T (3M + 4S).
+struct FoldSched {
+    uint32_t ndig, tail;      // nonzero digits; doublings after the last one
+    int8_t dig[64];           // signed odd digits, most significant first
+    uint8_t gap[64];          // doublings before dig[k] (gap[0] unused)
+};
+struct FoldArgs {
+    const ge *in[2];
+    ge *out[2];
+    uint32_t h, nseg;
+    uint32_t start[6], end[6], blk0[7];
+    uint32_t vec[6], sched[6];
+    FoldSched sc[4];
+};
+static void wnaf4_schedule(const ScD &k, FoldSched &s) {
+    // LSB-first width-4 NAF of the canonical scalar
+    int8_t d[260] = {0};
+    uint32_t x[9];
+    for (int i = 0; i < 8; i++) x[i] = k.v[i];
+    x[8] = 0;
+    int len = 0;
+    auto nz = [&]() { for (int i = 0; i < 9; i++) if (x[i]) return true; return false; };
+    while (nz() && len < 260) {
+        int di = 0;
+        if (x[0] & 1) {
+            di = (int)(x[0] & 15);
+            if (di >= 8) di -= 16;
+            // x -= di
+            if (di > 0) {
+                uint64_t bw = (uint64_t)di;
+                for (int i = 0; i < 9 && bw; i++) { uint64_t t = (uint64_t)x[i] - bw; x[i] = (uint32_t)t; bw = (t >> 63) & 1; }
             } else {
-                neg[bit >> 5] |= 1u << (bit & 31);
-                // k += 1
-                uint64_t c = 1;
-#pragma unroll
-                for (int i = 0; i < 9; i++) { c += k[i]; k[i] = (uint32_t)c; c >>= 32; }
+                uint64_t c = (uint64_t)(-di);
+                for (int i = 0; i < 9 && c; i++) { c += x[i]; x[i] = (uint32_t)c; c >>= 32; }
             }
-            top = bit;
         }
-        // k >>= 1
-#pragma unroll
-        for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
-        k[8] >>= 1;
+        d[len++] = (int8_t)di;
+        for (int i = 0; i < 8; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+        x[8] >>= 1;
     }
-    ge acc;
-    if (top < 0) {
-        acc = PL;
-    } else {
-        ge nPR;
-        ge_neg(nPR, PR);
-        acc = ((pos[top >> 5] >> (top & 31)) & 1) ? PR : nPR;
-        for (int bit = top - 1; bit >= 0; bit--) {
-            ge_dbl(acc, acc);
-            if ((pos[bit >> 5] >> (bit & 31)) & 1) ge_add(acc, acc, PR);
-            else if ((neg[bit >> 5] >> (bit & 31)) & 1) ge_add(acc, acc, nPR);
-        }
-        ge_add(acc, acc, PL);
+    s.ndig = 0; s.tail = 0;
+    int last = -1;
+    for (int pos = len - 1; pos >= 0; pos--) {
+        if (!d[pos]) continue;
+        if (s.ndig >= 64) throw HipError(hipErrorInvalidValue, "wnaf length", __FILE__, __LINE__);
+        s.dig[s.ndig] = d[pos];
+        s.gap[s.ndig] = (uint8_t)(last < 0 ? 0 : last - pos);
+        s.ndig++;
+        last = pos;
     }
-    out = acc;
+    s.tail = last < 0 ? 0 : (uint32_t)last;
 }
-__global__ void k_ipp_fold_points(const ge *__restrict__ Gin, const ge *__restrict__ Hin, uint32_t h, uint32_t n,
-                                  sc rGa, sc rGb, sc rHa, sc rHb, ge *__restrict__ Gout, ge *__restrict__ Hout) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * h) return;
-    bool isH = t >= h;
-    uint32_t i = isH ? t - h : t;
-    bool special = (i < n) && (h + i >= n);
-    const ge *P = isH ? Hin : Gin;
-    ge PL, PR, r;
-    ge_load(PL, P + i);
-    ge_load(PR, P + h + i);
-    const sc &rho = isH ? (special ? rHb : rHa) : (special ? rGb : rGa);
-    naf_mul_add(r, PL, PR, rho);
-    ge_store((isH ? Hout : Gout) + i, r);
+DEVI void fold_pick(gec &t, const gec &t1, const gec &t3, const gec &t5, const gec &t7, int d) {
+    int m = d < 0 ? -d : d;
+    if (m == 1) t = t1; else if (m == 3) t = t3; else if (m == 5) t = t5; else t = t7;
+}
+__global__ __launch_bounds__(64) void k_ipp_fold_points(const FoldArgs *__restrict__ Ap) {
+    const FoldArgs &A = *Ap;
+    uint32_t b = blockIdx.x, sg = 0;
+#pragma unroll
+    for (int k = 1; k < 6; k++) if (k < (int)A.nseg && b >= A.blk0[k]) sg = k;
+    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
+    if (i >= A.end[sg]) return;
+    const uint32_t v = A.vec[sg];
+    const FoldSched &S = A.sc[A.sched[sg]];
+    const ge *P = A.in[v];
+    ge PL, PR;
+    ge r;
+    if (S.ndig == 0) {
+        ge_load(PL, P + i);
+        r = PL;
+    } else {
+        ge_load(PR, P + A.h + i);
+        gec t1, t3, t5, t7;
+        ge p2, q;
+        ge_to_cached(t1, PR);
+        ge_dbl(p2, PR);
+        gec c2; ge_to_cached(c2, p2);
+        ge_add_c(q, PR, c2); ge_to_cached(t3, q);
+        ge_add_c(q, q, c2); ge_to_cached(t5, q);
+        ge_add_c(q, q, c2); ge_to_cached(t7, q);
+        ge acc;
+        {
+            gec t; fold_pick(t, t1, t3, t5, t7, S.dig[0]);
+            if (S.dig[0] < 0) gec_neg(t, t);
+            // acc = t as an extended point: X = (YpX - YmX)/2 etc. up to the common factor 2
+            fe_sub(acc.X, t.YpX, t.YmX);
+            fe_add(acc.Y, t.YpX, t.YmX);
+            acc.Z = t.Z2;
+            fe_mul(acc.T, acc.X, acc.Y);             // (2X)(2Y) = 2T * (2Z) / ... : rescale below
+            fe_mul(acc.X, acc.X, acc.Z);             // (2X:2Y:2Z) -> (4XZ:4YZ:4Z^2:4XY), T = XY/Z consistent
+            fe_mul(acc.Y, acc.Y, acc.Z);
+            fe_sq(acc.Z, acc.Z);
+        }
+        for (uint32_t k = 1; k < S.ndig; k++) {
+            const uint32_t g = S.gap[k];
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+            const int dk = S.dig[k];
+            gec t; fold_pick(t, t1, t3, t5, t7, dk);
+            if (dk > 0) ge_add_c(acc, acc, t); else ge_sub_c(acc, acc, t);
+        }
+        if (S.tail) {
+            for (uint32_t j = 1; j < S.tail; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        ge_load(PL, P + i);
+        ge_add(r, acc, PL);
+    }
+    ge_store(A.out[v] + i, r);
 }
 void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
-                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, hipStream_t st) {
-    hipLaunchKernelGGL(k_ipp_fold_points, dim3(nblk(2 * (uint64_t)h, 64)), dim3(64), 0, st, AS_CGE(Gin), AS_CGE(Hin),
-                       h, n, *reinterpret_cast<sc *>(&rhoG_a), *reinterpret_cast<sc *>(&rhoG_b),
-                       *reinterpret_cast<sc *>(&rhoH_a), *reinterpret_cast<sc *>(&rhoH_b), AS_GE(Gout), AS_GE(Hout));
+                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage, hipStream_t st) {
+    if (!stage.dev) {
+        BPG_HIP(hipMalloc(&stage.dev, sizeof(FoldArgs)));
+        BPG_HIP(hipHostMalloc(&stage.host, sizeof(FoldArgs), hipHostMallocDefault));
+    }
+    FoldArgs &A = *reinterpret_cast<FoldArgs *>(stage.host);
+    A = FoldArgs{};
+    A.in[0] = AS_CGE(Gin); A.in[1] = AS_CGE(Hin);
+    A.out[0] = AS_GE(Gout); A.out[1] = AS_GE(Hout);
+    A.h = h;
+    wnaf4_schedule(rhoG_a, A.sc[0]); wnaf4_schedule(rhoG_b, A.sc[1]);
+    wnaf4_schedule(rhoH_a, A.sc[2]); wnaf4_schedule(rhoH_b, A.sc[3]);
+    // lanes i < n <= h + i pair a real gate with padding and use rho_b
+    const uint32_t a = n > h ? std::min(n - h, h) : 0, bnd = std::min(n, h);
+    uint32_t blocks = 0;
+    for (uint32_t v = 0; v < 2; v++) {
+        const uint32_t lo[3] = {0, a, bnd}, hi[3] = {a, bnd, h}, cls[3] = {0, 1, 0};
+        for (int c = 0; c < 3; c++) {
+            if (hi[c] <= lo[c]) continue;
+            uint32_t k = A.nseg++;
+            A.start[k] = lo[c]; A.end[k] = hi[c]; A.vec[k] = v; A.sched[k] = 2 * v + cls[c];
+            A.blk0[k] = blocks;
+            blocks += nblk(hi[c] - lo[c], 64);
+        }
+    }
+    A.blk0[A.nseg] = blocks;
+    if (!blocks) return;
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldArgs), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_ipp_fold_points, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }
 __global__ void k_fill_scalars(sc *dst, sc val, uint32_t count) {

@@ -327,22 +327,20 @@ void ristretto_from_uniform(Point &p, const uint8_t b[64]) {
     pt_add(p, p1, p2);
 }
 
-static void fe_from_w(Fe &r, const uint32_t w[8]) {
-    uint8_t b[32];
-    for (int i = 0; i < 8; i++) { uint32_t x = w[i]; b[4 * i] = x; b[4 * i + 1] = x >> 8; b[4 * i + 2] = x >> 16; b[4 * i + 3] = x >> 24; }
-    // device values are < 2^256 (weakly reduced); fold bit 255 explicitly
-    uint32_t top = w[7] >> 31;
-    b[31] &= 0x7f;
-    ffrombytes(r, b);
-    r.v[0] += 19 * top;
+// Device field elements are 10 limbs of 26/25 bits (dev_field.h): limbs 2k
+// and 2k+1 are the low 26 and high 25 bits of radix-2^51 limb k. Device
+// limbs may carry a few bits over their width; fcarry absorbs that.
+static void fe_from_w(Fe &r, const uint32_t w[10]) {
+    for (int k = 0; k < 5; k++) r.v[k] = (uint64_t)w[2 * k] + ((uint64_t)w[2 * k + 1] << 26);
     fcarry(r);
 }
-static void fe_to_w(uint32_t w[8], const Fe &a) {
-    uint8_t b[32]; ftobytes(b, a);
-    for (int i = 0; i < 8; i++) w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+static void fe_to_w(uint32_t w[10], const Fe &a) {
+    Fe t = a;
+    fcarry(t);
+    for (int k = 0; k < 5; k++) { w[2 * k] = (uint32_t)(t.v[k] & 0x3ffffff); w[2 * k + 1] = (uint32_t)(t.v[k] >> 26); }
 }
-void pt_from_dev(Point &p, const uint32_t w[32]) { fe_from_w(p.X, w); fe_from_w(p.Y, w + 8); fe_from_w(p.Z, w + 16); fe_from_w(p.T, w + 24); }
-void pt_to_dev(uint32_t w[32], const Point &p) { fe_to_w(w, p.X); fe_to_w(w + 8, p.Y); fe_to_w(w + 16, p.Z); fe_to_w(w + 24, p.T); }
+void pt_from_dev(Point &p, const uint32_t w[40]) { fe_from_w(p.X, w); fe_from_w(p.Y, w + 10); fe_from_w(p.Z, w + 20); fe_from_w(p.T, w + 30); }
+void pt_to_dev(uint32_t w[40], const Point &p) { fe_to_w(w, p.X); fe_to_w(w + 10, p.Y); fe_to_w(w + 20, p.Z); fe_to_w(w + 30, p.T); }
 
 static const uint8_t BASEPOINT_COMPRESSED[32] = {
     0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9, 0x61, 0xc5, 0x00, 0x51, 0x5f,

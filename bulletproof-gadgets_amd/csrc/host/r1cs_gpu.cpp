@@ -115,7 +115,10 @@ struct Workspace {
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
+    dev::ArgStage fold_stage;        // IPP fold kernel arguments
     ~Workspace() {
+        if (fold_stage.dev) (void)hipFree(fold_stage.dev);
+        if (fold_stage.host) (void)hipHostFree(fold_stage.host);
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
@@ -550,7 +553,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
             Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
             PtD *Gn = as<PtD>(ws.Gp[k & 1]), *Hn = as<PtD>(ws.Hp[k & 1]);
             int pf = ws.prof_begin("ipp_fold_points", 6.0 * h * 64);
-            launch_ipp_fold_points(Gh, Hh, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn, st);
+            launch_ipp_fold_points(Gh, Hh, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn, ws.fold_stage, st);
             ws.prof_end(pf);
             Gh = Gn; Hh = Hn;
         }
