@@ -488,6 +488,17 @@ DEVI void ge_dbl_t(ge &r, const ge &p) {
 }
 DEVI void ge_dbl(ge &r, const ge &p) { ge_dbl_t<true>(r, p); }
 DEVI bool ge_is_identity(const ge &p) { return fe_iszero(p.X) || fe_iszero(p.Y); }
+// cached -> extended: (Y+X)-(Y-X) = 2X etc. give the projective (2X:2Y:2Z);
+// extend with (X'Z' : Y'Z' : Z'^2 : X'Y')  (3M + 1S)
+DEVI void ge_from_cached(ge &r, const gec &c) {
+    fe x, y;
+    fe_sub(x, c.YpX, c.YmX);
+    fe_add(y, c.YpX, c.YmX);
+    fe_mul(r.T, x, y);
+    fe_mul(r.X, x, c.Z2);
+    fe_mul(r.Y, y, c.Z2);
+    fe_sq(r.Z, c.Z2);
+}
 
 // RistrettoPoint::compress -> 8 canonical words
 DEVI void ristretto_encode(uint32_t out[8], const ge &p) {
@@ -584,6 +595,8 @@ DEVI void pt_store(P *dst, const P &p) {
 }
 DEVI void ge_load(ge &p, const ge *src) { pt_load(p, src); }
 DEVI void ge_store(ge *dst, const ge &p) { pt_store(dst, p); }
+DEVI void gec_load(gec &p, const gec *src) { pt_load(p, src); }
+DEVI void gec_store(gec *dst, const gec &p) { pt_store(dst, p); }
 DEVI void sc_load(sc &r, const sc *src) {
     const uint4 *s = reinterpret_cast<const uint4 *>(src);
     uint4 a = s[0], b = s[1];

@@ -28,6 +28,8 @@ struct HipError {
 };
 
 // -------------------------------------------------------------- points
+// Point arrays in HBM (generators, folded generators, decompressed inputs)
+// are cached points; MSM window rows returned to the host are extended.
 // out[i] = from_uniform_bytes(uniform[64*i .. 64*i+64))
 void launch_gens_map(const uint8_t *uniform, PtD *out, uint32_t count, hipStream_t st);
 // out[i] = v[i]*B + vb[i]*B_blinding using fixed-base tables (64 x 8 points each)
@@ -39,7 +41,7 @@ void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hi
 // -------------------------------------------------------------- MSM
 struct MsmSeg {
     const ScD *scal;   // canonical scalars (< l)
-    const PtD *base;   // extended points
+    const PtD *base;   // cached points (Y+X, Y-X, 2Z, 2dT)
     uint32_t count;
     uint32_t msm;      // which MSM of the job this segment contributes to
 };
@@ -72,7 +74,7 @@ class MsmEngine {
     void reserve(const MsmPlan &p);
     hipStream_t st_;
     DBuf keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_, cnt_, off_, E_, rk_a_, rk_b_, rp_a_, rp_b_, buckets_,
-        segacc_, rows_dev_;
+        bflag_, segacc_, rows_dev_;
 };
 
 // -------------------------------------------------------------- scalar vectors

@@ -18,19 +18,21 @@ namespace bpg {
 namespace dev {
 
 static_assert(sizeof(ScD) == sizeof(sc), "scalar layout");
-static_assert(sizeof(PtD) == sizeof(ge), "point layout");
+static_assert(sizeof(PtD) == sizeof(ge) && sizeof(PtD) == sizeof(gec), "point layout");
 
 #define AS_SC(p) reinterpret_cast<sc *>(p)
 #define AS_CSC(p) reinterpret_cast<const sc *>(p)
 #define AS_GE(p) reinterpret_cast<ge *>(p)
 #define AS_CGE(p) reinterpret_cast<const ge *>(p)
+#define AS_GEC(p) reinterpret_cast<gec *>(p)
+#define AS_CGEC(p) reinterpret_cast<const gec *>(p)
 
 static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // ===========================================================================
 // point kernels
 // ===========================================================================
-__global__ void k_gens_map(const uint32_t *__restrict__ uni, ge *__restrict__ out, uint32_t count) {
+__global__ __launch_bounds__(64) void k_gens_map(const uint32_t *__restrict__ uni, gec *__restrict__ out, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const uint32_t *w = uni + 16 * (size_t)i;
@@ -44,11 +46,12 @@ __global__ void k_gens_map(const uint32_t *__restrict__ uni, ge *__restrict__ ou
     ristretto_elligator(p1, r1);
     ristretto_elligator(p2, r2);
     ge_add(p, p1, p2);
-    ge_store(out + i, p);
+    gec c; ge_to_cached(c, p);
+    gec_store(out + i, c);
 }
 void launch_gens_map(const uint8_t *uniform, PtD *out, uint32_t count, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_gens_map, dim3(nblk(count, 128)), dim3(128), 0, st, (const uint32_t *)uniform, AS_GE(out), count);
+    hipLaunchKernelGGL(k_gens_map, dim3(nblk(count, 64)), dim3(64), 0, st, (const uint32_t *)uniform, AS_GEC(out), count);
     BPG_HIP(hipGetLastError());
 }
 
@@ -104,18 +107,19 @@ void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tab
     BPG_HIP(hipGetLastError());
 }
 
-__global__ void k_compress(const ge *__restrict__ in, uint32_t *__restrict__ out, uint32_t count) {
+__global__ __launch_bounds__(64) void k_compress(const gec *__restrict__ in, uint32_t *__restrict__ out, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    ge p; ge_load(p, in + i);
+    gec c; gec_load(c, in + i);
+    ge p; ge_from_cached(p, c);
     ristretto_encode(out + 8 * (size_t)i, p);
 }
 void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_compress, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGE(in), out, count);
+    hipLaunchKernelGGL(k_compress, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEC(in), out, count);
     BPG_HIP(hipGetLastError());
 }
-__global__ void k_decompress(const uint32_t *__restrict__ in, ge *__restrict__ out, int *ok, uint32_t count) {
+__global__ __launch_bounds__(64) void k_decompress(const uint32_t *__restrict__ in, gec *__restrict__ out, int *ok, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     uint32_t w[8];
@@ -124,20 +128,36 @@ __global__ void k_decompress(const uint32_t *__restrict__ in, ge *__restrict__ o
     ge p;
     bool good = ristretto_decode(p, w);
     if (!good) { ge_identity(p); atomicAnd(ok, 0); }
-    ge_store(out + i, p);
+    gec c; ge_to_cached(c, p);
+    gec_store(out + i, c);
 }
 void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_decompress, dim3(nblk(count, 64)), dim3(64), 0, st, in, AS_GE(out), ok, count);
+    hipLaunchKernelGGL(k_decompress, dim3(nblk(count, 64)), dim3(64), 0, st, in, AS_GEC(out), ok, count);
     BPG_HIP(hipGetLastError());
 }
 
 // ===========================================================================
 // Pippenger MSM
+//
+// Bases are cached points. One job = up to 8 (scalar, base) segments feeding
+// up to 2 MSMs. Signed c-bit windows give W digits per scalar; an entry
+// (key = row * half + |d| - 1, val = point | sign) per nonzero digit is
+// radix-sorted by key (hipcub), so each bucket is a contiguous run. Runs are
+// summed by fixed chunks of RBK_T entries per thread with keys/vals staged
+// through LDS (coalesced); a run that lies wholly inside one thread's chunk
+// goes straight to its bucket, runs that straddle chunks leave one partial
+// per chunk, which the next pass reduces the same way (pieces are sorted by
+// key). Buckets then fold into window rows (running sums per segment of
+// buckets + a weighted correction, then a block reduction per row); the host
+// combines rows with c doublings each.
 // ===========================================================================
+#define RBK_T 16
+#define RBK_BLOCK 256
+#define RBK_CHUNK (RBK_T * RBK_BLOCK)
 struct SegTab {
     const sc *scal[8];
-    const ge *base[8];
+    const gec *base[8];
     uint32_t gofs[9];
     uint32_t row0[8];
     int n;
@@ -180,73 +200,127 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t ha
     }
 }
 
-// run starts per chunk (first pass: E given on host; later: read from device)
-__global__ void k_rbk_count(const uint32_t *__restrict__ keys, uint64_t E_host, const uint32_t *E_dev, uint32_t T,
-                            uint32_t invalid, uint32_t nchunks, uint32_t *__restrict__ cnt) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nchunks) return;
-    uint64_t E = E_dev ? *E_dev : E_host;
-    uint64_t s = (uint64_t)j * T, e = s + T;
-    if (e > E) e = E;
-    uint32_t c = 0;
-    uint32_t prev = 0xffffffffu;
-    for (uint64_t i = s; i < e; i++) {
-        uint32_t k = keys[i];
-        if (k != invalid && (i == s || k != prev)) c++;
-        prev = k;
+// Stage one chunk of keys (and vals) into LDS with one pad word per RBK_T so
+// that thread t's entries t*T..t*T+T-1 sit at t*(T+1)+i (conflict-free).
+DEVI uint32_t rbk_lds(uint32_t j) { return j + j / RBK_T; }
+DEVI void rbk_stage(uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t base, uint64_t E, uint32_t invalid) {
+    for (uint32_t k = threadIdx.x; k < RBK_CHUNK; k += RBK_BLOCK) {
+        uint64_t idx = base + k;
+        sk[rbk_lds(k)] = idx < E ? keys[idx] : invalid;
     }
-    cnt[j] = (s < E) ? c : 0;
 }
-__global__ void k_rbk_total(const uint32_t *cnt, const uint32_t *off, uint32_t nchunks, uint32_t *E_out) {
-    *E_out = off[nchunks - 1] + cnt[nchunks - 1];
+DEVI uint64_t rbk_E(uint64_t E_host, const uint32_t *E_dev) { return E_dev ? *E_dev : E_host; }
+// key of the global entries just before / after this thread's chunk
+DEVI uint32_t rbk_prev_key(const uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t gstart, uint32_t t,
+                           uint32_t invalid) {
+    if (gstart == 0) return invalid;
+    return t ? sk[rbk_lds(t * RBK_T - 1)] : keys[gstart - 1];
+}
+DEVI uint32_t rbk_next_key(const uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t gend, uint64_t E,
+                           uint32_t t, uint32_t invalid) {
+    if (gend >= E) return invalid;
+    return (t + 1 < RBK_BLOCK) ? sk[rbk_lds((t + 1) * RBK_T)] : keys[gend];
 }
 
-DEVI void msm_gather(ge &p, const SegTab &T, uint32_t v) {
-    uint32_t g = v & 0x7fffffffu;
-    int si = seg_of(T, g);
-    ge_load(p, T.base[si] + (g - T.gofs[si]));
-    if (v >> 31) ge_neg(p, p);
-}
-// reduce consecutive equal keys inside each chunk; first pass gathers bases
-__global__ void k_rbk_sum(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
-                          const ge *__restrict__ pin, SegTab T, uint64_t E_host, const uint32_t *E_dev,
-                          uint32_t chunk, uint32_t invalid, uint32_t nchunks, const uint32_t *__restrict__ off,
-                          uint32_t *__restrict__ kout, ge *__restrict__ pout) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nchunks) return;
-    uint64_t E = E_dev ? *E_dev : E_host;
-    uint64_t s = (uint64_t)j * chunk, e = s + chunk;
-    if (s >= E) return;
-    if (e > E) e = E;
-    uint32_t o = off[j];
-    uint32_t cur = keys[s];
-    if (cur == invalid) return;
-    ge acc, p;
-    if (pin) ge_load(acc, pin + s); else msm_gather(acc, T, vals[s]);
-    for (uint64_t i = s + 1; i < e; i++) {
-        uint32_t k = keys[i];
-        if (k == invalid) break;
-        if (pin) ge_load(p, pin + i); else msm_gather(p, T, vals[i]);
-        if (k == cur) {
-            ge_add(acc, acc, p);
-        } else {
-            kout[o] = cur; ge_store(pout + o, acc); o++;
-            cur = k; acc = p;
+// pieces this thread leaves for the next pass (runs touching a chunk edge
+// that continue into a neighbour chunk)
+__global__ __launch_bounds__(RBK_BLOCK) void k_rbk_count(const uint32_t *__restrict__ keys, uint64_t E_host,
+                                                         const uint32_t *E_dev, uint32_t invalid,
+                                                         uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
+    const uint64_t E = rbk_E(E_host, E_dev);
+    const uint64_t base = (uint64_t)blockIdx.x * RBK_CHUNK;
+    const uint32_t t = threadIdx.x;
+    const uint32_t j = blockIdx.x * RBK_BLOCK + t;
+    if (base >= E) { cnt[j] = 0; return; }
+    rbk_stage(sk, keys, base, E, invalid);
+    __syncthreads();
+    const uint64_t gs = base + (uint64_t)t * RBK_T, ge_ = gs + RBK_T;
+    uint32_t c = 0;
+    if (gs < E) {
+        const uint32_t first = sk[rbk_lds(t * RBK_T)];
+        const uint32_t last = sk[rbk_lds(t * RBK_T + RBK_T - 1)];
+        const uint32_t pk = rbk_prev_key(sk, keys, gs, t, invalid);
+        const uint32_t nk = rbk_next_key(sk, keys, ge_, E, t, invalid);
+        if (first != invalid) {
+            const bool head_open = (pk == first), tail_open = (last != invalid) && (nk == last);
+            if (first == last) c = (head_open || tail_open) ? 1 : 0;
+            else c = (head_open ? 1 : 0) + (tail_open ? 1 : 0);
         }
     }
-    kout[o] = cur;
-    ge_store(pout + o, acc);
+    cnt[j] = c;
 }
-__global__ void k_fill_identity(ge *__restrict__ b, uint64_t n) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    ge id; ge_identity(id);
-    ge_store(b + i, id);
+__global__ void k_rbk_total(const uint32_t *cnt, const uint32_t *off, uint32_t nthreads, uint32_t *E_out) {
+    *E_out = off[nthreads - 1] + cnt[nthreads - 1];
 }
-// After the chunk passes a key can still straddle chunk boundaries (short
-// runs); the entry that starts a run sums the rest of it and owns the bucket.
-__global__ void k_scatter(const uint32_t *__restrict__ keys, const ge *__restrict__ pts, const uint32_t *E_dev,
-                          uint64_t cap, ge *__restrict__ buckets) {
+
+DEVI void msm_gather(gec &p, const SegTab &T, uint32_t v) {
+    uint32_t g = v & 0x7fffffffu;
+    int si = seg_of(T, g);
+    gec_load(p, T.base[si] + (g - T.gofs[si]));
+    gec_cneg(p, v >> 31);
+}
+// Sum runs. FIRST: entries are (key, signed base index); else entries are
+// pieces (key, extended partial at the same index) from the previous pass.
+template <bool FIRST>
+__global__ __launch_bounds__(RBK_BLOCK) void k_rbk_sum(const uint32_t *__restrict__ keys,
+                                                       const uint32_t *__restrict__ vals,
+                                                       const ge *__restrict__ pin, SegTab T, uint64_t E_host,
+                                                       const uint32_t *E_dev, uint32_t invalid,
+                                                       const uint32_t *__restrict__ off, uint32_t *__restrict__ kout,
+                                                       ge *__restrict__ pout, ge *__restrict__ buckets,
+                                                       uint8_t *__restrict__ bflag) {
+    __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
+    __shared__ uint32_t sv[FIRST ? RBK_CHUNK + RBK_BLOCK : 1];
+    const uint64_t E = rbk_E(E_host, E_dev);
+    const uint64_t base = (uint64_t)blockIdx.x * RBK_CHUNK;
+    if (base >= E) return;
+    const uint32_t t = threadIdx.x;
+    rbk_stage(sk, keys, base, E, invalid);
+    if (FIRST) {
+        for (uint32_t k = t; k < RBK_CHUNK; k += RBK_BLOCK) {
+            uint64_t idx = base + k;
+            sv[rbk_lds(k)] = idx < E ? vals[idx] : 0;
+        }
+    }
+    __syncthreads();
+    const uint64_t gs = base + (uint64_t)t * RBK_T;
+    if (gs >= E) return;
+    const uint32_t first = sk[rbk_lds(t * RBK_T)];
+    if (first == invalid) return;
+    const uint32_t pk = rbk_prev_key(sk, keys, gs, t, invalid);
+    const uint32_t nk = rbk_next_key(sk, keys, gs + RBK_T, E, t, invalid);
+    uint32_t o = off[blockIdx.x * RBK_BLOCK + t];
+    uint32_t cur = first;
+    bool open_start = (pk == first);     // the run being summed began in an earlier chunk
+    ge acc;
+    ge_identity(acc);
+    for (uint32_t i = 0; i < RBK_T; i++) {
+        const uint32_t k = sk[rbk_lds(t * RBK_T + i)];
+        if (k == invalid) break;
+        if (k != cur) {
+            if (open_start) { kout[o] = cur; ge_store(pout + o, acc); o++; }
+            else { ge_store(buckets + cur, acc); bflag[cur] = 1; }
+            cur = k; open_start = false;
+            ge_identity(acc);
+        }
+        if (FIRST) {
+            gec p; msm_gather(p, T, sv[rbk_lds(t * RBK_T + i)]);
+            ge_add_c(acc, acc, p);
+        } else {
+            ge p; ge_load(p, pin + gs + i);
+            ge_add(acc, acc, p);
+        }
+    }
+    // the last run is open if the next chunk continues it
+    if (open_start || nk == cur) { kout[o] = cur; ge_store(pout + o, acc); }
+    else { ge_store(buckets + cur, acc); bflag[cur] = 1; }
+}
+// After the last pass: a key may still have several pieces (giant runs);
+// the piece that starts the run sums the rest and owns the bucket.
+__global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
+                                                  const uint32_t *E_dev, uint64_t cap, ge *__restrict__ buckets,
+                                                  uint8_t *__restrict__ bflag) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t E = *E_dev;
     if (i >= cap || i >= E) return;
@@ -259,8 +333,9 @@ __global__ void k_scatter(const uint32_t *__restrict__ keys, const ge *__restric
         ge_add(acc, acc, p);
     }
     ge_store(buckets + k, acc);
+    bflag[k] = 1;
 }
-// sum_{b in seg} (b+1) * S_b = acc + lo * run, with acc weights 1..seglen
+// r = k * p for small k (weights of bucket segments)
 DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {
     ge_identity(r);
     if (!k) return;
@@ -271,18 +346,23 @@ DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {
         if ((k >> b) & 1) ge_add(r, r, p);
     }
 }
-__global__ void k_bucket_seg(const ge *__restrict__ buckets, uint32_t rows, uint32_t half, uint32_t seglen,
-                             uint32_t nseg, ge *__restrict__ segacc) {
+DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict__ F, uint32_t i) {
+    if (F[i]) ge_load(p, B + i); else ge_identity(p);
+}
+// sum_{b in seg} (b+1) * S_b = acc + lo * run, with acc weights 1..seglen
+__global__ __launch_bounds__(64) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
+                                                   uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
+                                                   ge *__restrict__ segacc) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= rows * nseg) return;
     uint32_t row = t / nseg, s = t % nseg;
     uint32_t lo = s * seglen;
-    const ge *B = buckets + (size_t)row * half + lo;
+    const size_t b0 = (size_t)row * half + lo;
     ge run, acc, p;
-    ge_load(run, B + seglen - 1);
+    bucket_load(run, buckets + b0, bflag + b0, seglen - 1);
     acc = run;
     for (int b = (int)seglen - 2; b >= 0; b--) {
-        ge_load(p, B + b);
+        bucket_load(p, buckets + b0, bflag + b0, b);
         ge_add(run, run, p);
         ge_add(acc, acc, run);
     }
@@ -324,7 +404,7 @@ static int msm_window(uint64_t total) {
 
 MsmEngine::~MsmEngine() {
     DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &scan_tmp_, &cnt_, &off_, &E_,
-                    &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &segacc_, &rows_dev_};
+                    &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &bflag_, &segacc_, &rows_dev_};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
 }
@@ -343,12 +423,13 @@ void MsmEngine::reserve(const MsmPlan &p) {
     keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
     sort_tmp_.grow(p.sort_tmp);
     scan_tmp_.grow(p.scan_tmp);
-    uint64_t nch = (p.E0 + p.T - 1) / p.T + 1;
-    cnt_.grow(nch * 4); off_.grow(nch * 4);
+    uint64_t nthr = ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK + 1;
+    cnt_.grow(nthr * 4); off_.grow(nthr * 4);
     E_.grow(64 * 4);
     rk_a_.grow(p.capE * 4); rk_b_.grow(p.capE * 4);
     rp_a_.grow(p.capE * sizeof(ge)); rp_b_.grow(p.capE * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
+    bflag_.grow((size_t)p.rows * p.half);
     segacc_.grow((size_t)p.rows * p.nseg_per_row * sizeof(ge));
     rows_dev_.grow((size_t)p.rows * sizeof(ge));
 }
@@ -369,44 +450,44 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     p.half = 1 << (p.c - 1);
     for (int i = 0; i < nseg; i++) {
         T.scal[i] = AS_CSC(segs[i].scal);
-        T.base[i] = AS_CGE(segs[i].base);
+        T.base[i] = AS_CGEC(segs[i].base);
         T.row0[i] = segs[i].msm * p.W;
     }
     p.E0 = (uint64_t)p.W * total;
-    p.T = 32;
+    p.T = RBK_T;
     uint64_t D = (uint64_t)p.rows * p.half;
     uint32_t invalid = (uint32_t)D;
     p.key_bits = 1;
     while ((1ULL << p.key_bits) <= D) p.key_bits++;
-    p.capE = std::min<uint64_t>(p.E0, D + (p.E0 + p.T - 1) / p.T + 1);
+    // pieces after a pass: at most 2 per thread chunk
+    p.capE = std::min<uint64_t>(p.E0, 2 * ((p.E0 + RBK_T - 1) / RBK_T) + 2);
     // passes: enough that T^passes exceeds the largest possible run (total)
     p.passes = 1;
-    { uint64_t r = p.T; while (r < total + 1) { r *= p.T; p.passes++; } }
-    p.passes += 1;
+    { uint64_t r = RBK_T / 2; while (r < total + 1) { r *= RBK_T / 2; p.passes++; } }
     p.seglen = p.half < 16 ? p.half : 16;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
         for (int r = 0; r < p.rows; r++) {
-            ge id;
             uint32_t *w = reinterpret_cast<uint32_t *>(&rows_host[r]);
             memset(w, 0, sizeof(PtD)); w[10] = 1; w[20] = 1;
-            (void)id;
         }
         return p;
     }
-    // temp sizes
     {
         size_t s = 0;
         (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                            (uint32_t *)nullptr, (int)p.E0, 0, (int)p.key_bits, st_);
         p.sort_tmp = s;
         size_t s2 = 0;
-        uint64_t nch = (p.E0 + p.T - 1) / p.T;
-        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nch, st_);
+        uint64_t nthr = ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nthr, st_);
         p.scan_tmp = s2;
     }
     reserve(p);
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
+    uint8_t *bflag = (uint8_t *)bflag_.p;
+    ge *buckets = AS_GE(buckets_.p);
+    BPG_HIP(hipMemsetAsync(bflag, 0, D, st_));
     hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
                        (uint32_t)p.half, invalid, keys, vals);
     BPG_HIP(hipGetLastError());
@@ -421,16 +502,20 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     uint64_t Ebound = p.E0;
     const uint32_t *Ein = nullptr;
     for (int pass = 0; pass < p.passes; pass++) {
-        uint32_t nch = (uint32_t)((Ebound + p.T - 1) / p.T);
-        if (nch == 0) nch = 1;
-        hipLaunchKernelGGL(k_rbk_count, dim3(nblk(nch, 256)), dim3(256), 0, st_, kin, Ebound, Ein, p.T, invalid, nch, cnt);
+        uint32_t nblocks = (uint32_t)((Ebound + RBK_CHUNK - 1) / RBK_CHUNK);
+        if (nblocks == 0) nblocks = 1;
+        uint32_t nthr = nblocks * RBK_BLOCK;
+        hipLaunchKernelGGL(k_rbk_count, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, Ebound, Ein, invalid, cnt);
         size_t tb = p.scan_tmp;
-        BPG_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp_.p, tb, cnt, off, (int)nch, st_));
-        hipLaunchKernelGGL(k_rbk_total, dim3(1), dim3(1), 0, st_, cnt, off, nch, Ed + pass);
-        hipLaunchKernelGGL(k_rbk_sum, dim3(nblk(nch, 64)), dim3(64), 0, st_, kin, (const uint32_t *)vals2, pin, T,
-                           Ebound, Ein, p.T, invalid, nch, off, kout, pout);
+        BPG_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp_.p, tb, cnt, off, (int)nthr, st_));
+        hipLaunchKernelGGL(k_rbk_total, dim3(1), dim3(1), 0, st_, cnt, off, nthr, Ed + pass);
+        if (pass == 0)
+            hipLaunchKernelGGL(k_rbk_sum<true>, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, (const uint32_t *)vals2,
+                               pin, T, Ebound, Ein, invalid, off, kout, pout, buckets, bflag);
+        else
+            hipLaunchKernelGGL(k_rbk_sum<false>, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, (const uint32_t *)vals2,
+                               pin, T, Ebound, Ein, invalid, off, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
-        // next pass reads this output
         Ein = Ed + pass;
         Ebound = std::min<uint64_t>(Ebound, p.capE);
         kin = kout;
@@ -438,11 +523,11 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         kout = (kout == (uint32_t *)rk_a_.p) ? (uint32_t *)rk_b_.p : (uint32_t *)rk_a_.p;
         pout = (pout == AS_GE(rp_a_.p)) ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
     }
-    hipLaunchKernelGGL(k_fill_identity, dim3(nblk(D, 256)), dim3(256), 0, st_, AS_GE(buckets_.p), D);
-    hipLaunchKernelGGL(k_scatter, dim3(nblk(Ebound, 256)), dim3(256), 0, st_, kin, pin, Ein, Ebound, AS_GE(buckets_.p));
+    hipLaunchKernelGGL(k_rbk_final, dim3(nblk(Ebound, 64)), dim3(64), 0, st_, kin, pin, Ein, Ebound, buckets, bflag);
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
-    hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), (uint32_t)p.rows,
-                       (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, AS_GE(segacc_.p));
+    hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
+                       (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row,
+                       AS_GE(segacc_.p));
     hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, AS_CGE(segacc_.p), (uint32_t)p.nseg_per_row,
                        AS_GE(rows_dev_.p));
     BPG_HIP(hipGetLastError());
@@ -762,8 +847,8 @@ struct FoldSched {
     uint8_t gap[64];          // doublings before dig[k] (gap[0] unused)
 };
 struct FoldArgs {
-    const ge *in[2];
-    ge *out[2];
+    const gec *in[2];
+    gec *out[2];
     uint32_t h, nseg;
     uint32_t start[6], end[6], blk0[7];
     uint32_t vec[6], sched[6];
@@ -820,51 +905,48 @@ __global__ __launch_bounds__(64) void k_ipp_fold_points(const FoldArgs *__restri
     if (i >= A.end[sg]) return;
     const uint32_t v = A.vec[sg];
     const FoldSched &S = A.sc[A.sched[sg]];
-    const ge *P = A.in[v];
-    ge PL, PR;
-    ge r;
+    const gec *P = A.in[v];
+    gec PL;
     if (S.ndig == 0) {
-        ge_load(PL, P + i);
-        r = PL;
-    } else {
-        ge_load(PR, P + A.h + i);
-        gec t1, t3, t5, t7;
-        ge p2, q;
-        ge_to_cached(t1, PR);
-        ge_dbl(p2, PR);
+        gec_load(PL, P + i);
+        gec_store(A.out[v] + i, PL);
+        return;
+    }
+    gec t1, t3, t5, t7;
+    {
+        gec_load(t1, P + A.h + i);
+        ge pr, p2, q;
+        fe_sub(pr.X, t1.YpX, t1.YmX);            // projective (2X : 2Y : 2Z), enough to double
+        fe_add(pr.Y, t1.YpX, t1.YmX);
+        pr.Z = t1.Z2;
+        ge_dbl(p2, pr);
         gec c2; ge_to_cached(c2, p2);
-        ge_add_c(q, PR, c2); ge_to_cached(t3, q);
+        ge_add_c(q, p2, t1); ge_to_cached(t3, q);
         ge_add_c(q, q, c2); ge_to_cached(t5, q);
         ge_add_c(q, q, c2); ge_to_cached(t7, q);
-        ge acc;
-        {
-            gec t; fold_pick(t, t1, t3, t5, t7, S.dig[0]);
-            if (S.dig[0] < 0) gec_neg(t, t);
-            // acc = t as an extended point: X = (YpX - YmX)/2 etc. up to the common factor 2
-            fe_sub(acc.X, t.YpX, t.YmX);
-            fe_add(acc.Y, t.YpX, t.YmX);
-            acc.Z = t.Z2;
-            fe_mul(acc.T, acc.X, acc.Y);             // (2X)(2Y) = 2T * (2Z) / ... : rescale below
-            fe_mul(acc.X, acc.X, acc.Z);             // (2X:2Y:2Z) -> (4XZ:4YZ:4Z^2:4XY), T = XY/Z consistent
-            fe_mul(acc.Y, acc.Y, acc.Z);
-            fe_sq(acc.Z, acc.Z);
-        }
-        for (uint32_t k = 1; k < S.ndig; k++) {
-            const uint32_t g = S.gap[k];
-            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
-            ge_dbl_t<true>(acc, acc);
-            const int dk = S.dig[k];
-            gec t; fold_pick(t, t1, t3, t5, t7, dk);
-            if (dk > 0) ge_add_c(acc, acc, t); else ge_sub_c(acc, acc, t);
-        }
-        if (S.tail) {
-            for (uint32_t j = 1; j < S.tail; j++) ge_dbl_t<false>(acc, acc);
-            ge_dbl_t<true>(acc, acc);
-        }
-        ge_load(PL, P + i);
-        ge_add(r, acc, PL);
     }
-    ge_store(A.out[v] + i, r);
+    ge acc;
+    {
+        gec t; fold_pick(t, t1, t3, t5, t7, S.dig[0]);
+        if (S.dig[0] < 0) gec_neg(t, t);
+        ge_from_cached(acc, t);
+    }
+    for (uint32_t k = 1; k < S.ndig; k++) {
+        const uint32_t g = S.gap[k];
+        for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+        ge_dbl_t<true>(acc, acc);
+        const int dk = S.dig[k];
+        gec t; fold_pick(t, t1, t3, t5, t7, dk);
+        if (dk > 0) ge_add_c(acc, acc, t); else ge_sub_c(acc, acc, t);
+    }
+    if (S.tail) {
+        for (uint32_t j = 1; j < S.tail; j++) ge_dbl_t<false>(acc, acc);
+        ge_dbl_t<true>(acc, acc);
+    }
+    gec_load(PL, P + i);
+    ge r; ge_add_c(r, acc, PL);
+    gec out; ge_to_cached(out, r);
+    gec_store(A.out[v] + i, out);
 }
 void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
                             ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage, hipStream_t st) {
@@ -874,8 +956,8 @@ void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t
     }
     FoldArgs &A = *reinterpret_cast<FoldArgs *>(stage.host);
     A = FoldArgs{};
-    A.in[0] = AS_CGE(Gin); A.in[1] = AS_CGE(Hin);
-    A.out[0] = AS_GE(Gout); A.out[1] = AS_GE(Hout);
+    A.in[0] = AS_CGEC(Gin); A.in[1] = AS_CGEC(Hin);
+    A.out[0] = AS_GEC(Gout); A.out[1] = AS_GEC(Hout);
     A.h = h;
     wnaf4_schedule(rhoG_a, A.sc[0]); wnaf4_schedule(rhoG_b, A.sc[1]);
     wnaf4_schedule(rhoH_a, A.sc[2]); wnaf4_schedule(rhoH_b, A.sc[3]);

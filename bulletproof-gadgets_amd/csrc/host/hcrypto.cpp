@@ -341,6 +341,11 @@ static void fe_to_w(uint32_t w[10], const Fe &a) {
 }
 void pt_from_dev(Point &p, const uint32_t w[40]) { fe_from_w(p.X, w); fe_from_w(p.Y, w + 10); fe_from_w(p.Z, w + 20); fe_from_w(p.T, w + 30); }
 void pt_to_dev(uint32_t w[40], const Point &p) { fe_to_w(w, p.X); fe_to_w(w + 10, p.Y); fe_to_w(w + 20, p.Z); fe_to_w(w + 30, p.T); }
+void pt_to_dev_cached(uint32_t w[40], const Point &p) {
+    Fe ypx, ymx, z2, t2d;
+    fadd(ypx, p.Y, p.X); fsub(ymx, p.Y, p.X); fadd(z2, p.Z, p.Z); fmul(t2d, p.T, FD2);
+    fe_to_w(w, ypx); fe_to_w(w + 10, ymx); fe_to_w(w + 20, z2); fe_to_w(w + 30, t2d);
+}
 
 static const uint8_t BASEPOINT_COMPRESSED[32] = {
     0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9, 0x61, 0xc5, 0x00, 0x51, 0x5f,

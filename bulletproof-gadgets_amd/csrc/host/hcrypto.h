@@ -56,6 +56,7 @@ void ristretto_from_uniform(Point &p, const uint8_t b[64]);
 // conversion from/to the device layout (8 x 32-bit limbs per coordinate)
 void pt_from_dev(Point &p, const uint32_t w[40]);   // device layout, dev_field.h
 void pt_to_dev(uint32_t w[40], const Point &p);
+void pt_to_dev_cached(uint32_t w[40], const Point &p);   // (Y+X, Y-X, 2Z, 2dT)
 // PedersenGens::default() with fixed-base tables
 const Point &basepoint_B();
 const Point &basepoint_B_blinding();

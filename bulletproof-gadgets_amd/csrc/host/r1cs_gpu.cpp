@@ -501,7 +501,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     Scalar wch = T.challenge_scalar("w");
     Point Qp; mul_B(Qp, wch);
     ws.Q.grow(sizeof(PtD));
-    PtD Qd; pt_to_dev(Qd.v, Qp);
+    PtD Qd; pt_to_dev_cached(Qd.v, Qp);
     BPG_HIP(hipMemcpyAsync(ws.Q.p, &Qd, sizeof(PtD), hipMemcpyHostToDevice, st));
     ws.a.grow((size_t)N * sizeof(ScD) + 64);
     ws.b.grow((size_t)N * sizeof(ScD) + 64);

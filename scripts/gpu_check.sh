@@ -8,7 +8,7 @@ timeout -k 10 600 python bench.py > gpurun_out/${R}_bench.json 2> gpurun_out/${R
 if [ "${PROF:-1}" = 1 ]; then
   ROOTD=$(pwd)
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOTD/gpurun_out/${R}_prof -o run -- python3 $ROOTD/bench.py --steps 2 --no-cpu-baseline > $ROOTD/gpurun_out/${R}_prof_bench.json 2> $ROOTD/gpurun_out/${R}_prof.err
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOTD/gpurun_out/${R}_prof -o run -- python3 $ROOTD/bench.py --steps 2 --threads ${PROF_THREADS:-2} --batch ${PROF_BATCH:-4} --no-cpu-baseline > $ROOTD/gpurun_out/${R}_prof_bench.json 2> $ROOTD/gpurun_out/${R}_prof.err
   cd $ROOTD
 fi
 echo done
