@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 2 x threads)")
+    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 8 x threads)")
     ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (default min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
@@ -91,7 +91,7 @@ def main():
     ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
     threads = a.threads or max(1, min(16, ncpu // max(world, 1) if world > 1 else ncpu))
     threads = min(threads, 16)
-    batch = a.batch or 2 * threads
+    batch = a.batch or 8 * threads
 
     inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * rank)
     bpg.set_seed(1000 + rank)

@@ -24,7 +24,8 @@ EXPORTS = [
     "bpg_pedersen_commit", "bpg_r1cs_prove", "bpg_r1cs_verify", "bpg_prepare", "bpg_prepared_free",
     "bpg_prove_batch", "bpg_last_timings", "bpg_msm", "bpg_synthesize", "bpg_synthesize_verifier",
     "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free", "bpg_mimc_hash",
-    "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset",
+    "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
+    "bpg_rng_rate",
 ]
 
 
@@ -89,6 +90,8 @@ def lib():
         L.bpg_synth_V.restype = vp
         L.bpg_synth_V.argtypes = [vp]
         L.bpg_synth_free.argtypes = [vp]
+        L.bpg_rng_rate.restype = ctypes.c_double
+        L.bpg_rng_rate.argtypes = [u32, ctypes.c_int]
         _lib = L
     return _lib
 

@@ -1,0 +1,54 @@
+// fold_bench.hip — isolated timing of the IPP point fold (k_ipp_fold_points)
+// and one MSM job at the config-5 round-0 size, for occupancy/variant
+// experiments. Points come from the generator map on random bytes.
+#include "../device/kernels.hip"
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+using namespace bpg::dev;
+int main(int argc, char **argv) {
+    uint32_t h = argc > 1 ? atoi(argv[1]) : (1u << 19);
+    uint32_t n = argc > 2 ? atoi(argv[2]) : 744712 / 2;
+    std::vector<uint8_t> uni((size_t)2 * h * 64);
+    srand(1);
+    for (auto &b : uni) b = rand() & 255;
+    uint8_t *duni; PtD *G, *H, *Go, *Ho;
+    BPG_HIP(hipMalloc(&duni, uni.size()));
+    BPG_HIP(hipMemcpy(duni, uni.data(), uni.size(), hipMemcpyHostToDevice));
+    BPG_HIP(hipMalloc(&G, (size_t)2 * h * sizeof(PtD))); BPG_HIP(hipMalloc(&H, (size_t)2 * h * sizeof(PtD)));
+    BPG_HIP(hipMalloc(&Go, (size_t)h * sizeof(PtD))); BPG_HIP(hipMalloc(&Ho, (size_t)h * sizeof(PtD)));
+    launch_gens_map(duni, G, 2 * h, 0);
+    launch_gens_map(duni, H, 2 * h, 0);
+    BPG_HIP(hipDeviceSynchronize());
+    ScD r[4];
+    for (int k = 0; k < 4; k++) { for (int i = 0; i < 8; i++) r[k].v[i] = rand() * 2654435761u; r[k].v[7] &= 0x0fffffff; }
+    ArgStage stage;
+    hipStream_t st; BPG_HIP(hipStreamCreate(&st));
+    hipEvent_t e0, e1; BPG_HIP(hipEventCreate(&e0)); BPG_HIP(hipEventCreate(&e1));
+    launch_ipp_fold_points(G, H, h, n, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
+    BPG_HIP(hipStreamSynchronize(st));
+    const int reps = 3;
+    BPG_HIP(hipEventRecord(e0, st));
+    for (int k = 0; k < reps; k++) launch_ipp_fold_points(G, H, h, n, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
+    BPG_HIP(hipEventRecord(e1, st));
+    BPG_HIP(hipEventSynchronize(e1));
+    float ms; BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
+    printf("fold h=%u (2h=%u lanes): %.3f ms per launch, %.1f ns per lane\n", h, 2 * h, ms / reps, ms / reps * 1e6 / (2.0 * h));
+    // one MSM job: 4 segments of h points (round-0 L/R shape)
+    std::vector<ScD> sc((size_t)4 * h);
+    for (auto &s : sc) { for (int i = 0; i < 8; i++) s.v[i] = rand() * 2654435761u + rand(); s.v[7] &= 0x0fffffff; }
+    ScD *dsc; BPG_HIP(hipMalloc(&dsc, sc.size() * sizeof(ScD)));
+    BPG_HIP(hipMemcpy(dsc, sc.data(), sc.size() * sizeof(ScD), hipMemcpyHostToDevice));
+    MsmEngine eng(st);
+    PtD *rows; BPG_HIP(hipHostMalloc((void **)&rows, 128 * sizeof(PtD), hipHostMallocDefault));
+    MsmSeg seg[4] = {{dsc, G + h, h, 0}, {dsc + h, H, h, 0}, {dsc + 2 * (size_t)h, G, h, 1}, {dsc + 3 * (size_t)h, H + h, h, 1}};
+    eng.enqueue(seg, 4, 2, rows);
+    BPG_HIP(hipStreamSynchronize(st));
+    BPG_HIP(hipEventRecord(e0, st));
+    for (int k = 0; k < reps; k++) eng.enqueue(seg, 4, 2, rows);
+    BPG_HIP(hipEventRecord(e1, st));
+    BPG_HIP(hipEventSynchronize(e1));
+    BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
+    printf("msm job 4h=%u points: %.3f ms per job\n", 4 * h, ms / reps);
+    return 0;
+}

@@ -78,6 +78,8 @@ class MsmEngine {
 };
 
 // -------------------------------------------------------------- scalar vectors
+// out[i] = from_bytes_mod_order_wide(wide[64 i .. 64 i + 64)) (canonical)
+void launch_wide_reduce(const uint8_t *wide, uint32_t count, ScD *out, hipStream_t st);
 // out[i] = base^(start + i) for i < count, given base2[b] = base^(2^b), b < 32
 void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out, hipStream_t st);
 // out[i] = lo[i & 1023] * hi[i >> 10]

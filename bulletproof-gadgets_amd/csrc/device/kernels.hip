@@ -541,6 +541,29 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
 DEVI void mm(sc &r, const sc &a, const sc &b) { sc_montmul(r, a, b); }
 DEVI sc sc_one_raw() { sc o; sc_zero(o); o.v[0] = 1; return o; }
 
+// Scalar::from_bytes_mod_order_wide of raw 64-byte TranscriptRng draws:
+// lo + hi * 2^256 mod l, with hi * 2^256 = montmul(hi, R^2).
+__global__ void k_wide_reduce(const uint32_t *__restrict__ wide, uint32_t count, sc *__restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint4 *w = reinterpret_cast<const uint4 *>(wide + 16 * (size_t)i);
+    uint4 q0 = w[0], q1 = w[1], q2 = w[2], q3 = w[3];
+    sc lo, hi, r2, a, b;
+    lo.v[0] = q0.x; lo.v[1] = q0.y; lo.v[2] = q0.z; lo.v[3] = q0.w; lo.v[4] = q1.x; lo.v[5] = q1.y; lo.v[6] = q1.z; lo.v[7] = q1.w;
+    hi.v[0] = q2.x; hi.v[1] = q2.y; hi.v[2] = q2.z; hi.v[3] = q2.w; hi.v[4] = q3.x; hi.v[5] = q3.y; hi.v[6] = q3.z; hi.v[7] = q3.w;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r2.v[k] = SC_R2[k];
+    sc_reduce(a, lo);
+    sc_montmul(b, hi, r2);
+    sc_add(a, a, b);
+    sc_store(out + i, a);
+}
+void launch_wide_reduce(const uint8_t *wide, uint32_t count, ScD *out, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_wide_reduce, dim3(nblk(count, 256)), dim3(256), 0, st, (const uint32_t *)wide, count, AS_SC(out));
+    BPG_HIP(hipGetLastError());
+}
+
 // out[i] = mont(base^(start+i)); base2[b] = mont(base^(2^b))
 __global__ void k_pow_table(const sc *__restrict__ base2, uint64_t start, uint32_t count, sc *__restrict__ out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -896,7 +919,10 @@ DEVI void fold_pick(gec &t, const gec &t1, const gec &t3, const gec &t5, const g
     int m = d < 0 ? -d : d;
     if (m == 1) t = t1; else if (m == 3) t = t3; else if (m == 5) t = t5; else t = t7;
 }
-__global__ __launch_bounds__(64) void k_ipp_fold_points(const FoldArgs *__restrict__ Ap) {
+#ifndef BPG_FOLD_WAVES
+#define BPG_FOLD_WAVES 1
+#endif
+__global__ __launch_bounds__(64, BPG_FOLD_WAVES) void k_ipp_fold_points(const FoldArgs *__restrict__ Ap) {
     const FoldArgs &A = *Ap;
     uint32_t b = blockIdx.x, sg = 0;
 #pragma unroll

@@ -6,6 +6,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
+#include <deque>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -237,35 +239,152 @@ struct Pool {
 Pool &pool() { static Pool *p = new Pool(); return *p; }
 }  // namespace
 
+// Batched proving as a two-stage pipeline: producer threads
+// draw the TranscriptRng streams of 8 proofs at a time in lockstep (rng8)
+// into pinned slots, consumer threads drive the device part of each proof
+// on their own HIP stream. The RNG phase of later proofs overlaps the device
+// phase of earlier ones instead of alternating with it.
 int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, const uint8_t *entropy, uint32_t count,
                     uint32_t threads, uint8_t *proof_out, size_t proof_stride, size_t *lens) {
     return guarded([&]() -> int {
+        if (!count) return 0;
+        const PreparedCS &cs = *p->p;
+        if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
         if (threads == 0) threads = 1;
-        if (threads > count) threads = count ? count : 1;
-        std::atomic<uint32_t> next(0);
-        std::mutex emu;
+        uint32_t groups = (count + 7) / 8;
+        // producers: ~half the threads (one lockstep group of 8 each); slots
+        // (device buffers) for the groups being drawn plus a queue per consumer
+        uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(groups, threads / 2));
+        uint32_t C = std::max<uint32_t>(1, std::min<uint32_t>(count, threads > P ? threads - P : 1));
+        uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
+        std::vector<uint8_t *> slot = cs.slots(nslots, 2 * (size_t)cs.n * 64 + 64);
+        std::mutex mu;
+        std::condition_variable cv;
+        std::vector<int> free_slots;
+        for (uint32_t i = 0; i < nslots; i++) free_slots.push_back((int)i);
+        std::vector<RngBlock> blocks(count);
+        std::deque<uint32_t> ready;
+        std::atomic<uint32_t> next_group(0);
+        uint32_t producers_left = P;
+        bool abort = false;
         std::string err;
-        pool().run((int)threads, [&](int) {
+        auto fail = [&](const std::string &e) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (err.empty()) err = e;
+            abort = true;
+            cv.notify_all();
+        };
+        std::vector<int> slot_of(count, -1);
+        pool().run((int)(P + C), [&](int id) {
             try {
-                for (;;) {
-                    uint32_t k = next.fetch_add(1);
-                    if (k >= count) break;
-                    std::vector<uint8_t> pr = gpu_prove(*p->p, label, label_len, entropy + 32 * (size_t)k);
-                    if (pr.size() > proof_stride) throw std::runtime_error("proof stride too small");
-                    memcpy(proof_out + proof_stride * (size_t)k, pr.data(), pr.size());
-                    lens[k] = pr.size();
+                if ((uint32_t)id < P) {
+                    for (;;) {
+                        uint32_t g = next_group.fetch_add(1);
+                        if (g >= groups) break;
+                        uint32_t k0 = 8 * g, cnt = std::min<uint32_t>(8, count - k0);
+                        {
+                            std::unique_lock<std::mutex> lk(mu);
+                            cv.wait(lk, [&] { return abort || free_slots.size() >= cnt; });
+                            if (abort) break;
+                            for (uint32_t i = 0; i < cnt; i++) {
+                                slot_of[k0 + i] = free_slots.back();
+                                free_slots.pop_back();
+                            }
+                        }
+                        const uint8_t *ent[8];
+                        RngBlock *out[8];
+                        for (uint32_t i = 0; i < cnt; i++) {
+                            ent[i] = entropy + 32 * (size_t)(k0 + i);
+                            blocks[k0 + i].wide = slot[slot_of[k0 + i]];
+                            blocks[k0 + i].on_device = true;
+                            out[i] = &blocks[k0 + i];
+                        }
+                        rng_draw_group(cs, label, label_len, ent, (int)cnt, out, true);
+                        std::lock_guard<std::mutex> lk(mu);
+                        for (uint32_t i = 0; i < cnt; i++) ready.push_back(k0 + i);
+                        cv.notify_all();
+                    }
+                    std::lock_guard<std::mutex> lk(mu);
+                    producers_left--;
+                    cv.notify_all();
+                } else {
+                    for (;;) {
+                        uint32_t k;
+                        {
+                            std::unique_lock<std::mutex> lk(mu);
+                            cv.wait(lk, [&] { return abort || !ready.empty() || producers_left == 0; });
+                            if (abort || ready.empty()) break;
+                            k = ready.front();
+                            ready.pop_front();
+                        }
+                        std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, blocks[k]);
+                        if (pr.size() > proof_stride) throw std::runtime_error("proof stride too small");
+                        memcpy(proof_out + proof_stride * (size_t)k, pr.data(), pr.size());
+                        lens[k] = pr.size();
+                        std::lock_guard<std::mutex> lk(mu);
+                        free_slots.push_back(slot_of[k]);
+                        cv.notify_all();
+                    }
                 }
             } catch (const dev::HipError &e) {
-                std::lock_guard<std::mutex> lk(emu);
-                err = std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr;
+                fail(std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr);
             } catch (const std::exception &e) {
-                std::lock_guard<std::mutex> lk(emu);
-                err = e.what();
+                fail(e.what());
             }
         });
         if (!err.empty()) throw std::runtime_error(err);
         return 0;
     }, -1);
+}
+
+// Diagnostics: lockstep RNG against the scalar TranscriptRng (0 = equal),
+// and its draw rate (draws per second per thread for `lanes` proofs).
+int bpg_rng_selftest(void) {
+    return guarded([&]() -> int {
+        Transcript T((const uint8_t *)"selftest", 8);
+        T.append_u64("m", 3);
+        TranscriptRng base(T);
+        base.rekey_with_witness_bytes("v_blinding", (const uint8_t *)"0123456789abcdef0123456789abcdef", 32);
+        for (int lanes = 1; lanes <= 8; lanes++) {
+            uint8_t ent[8][32];
+            const uint8_t *ep[8];
+            for (int k = 0; k < 8; k++) { for (int i = 0; i < 32; i++) ent[k][i] = (uint8_t)(k * 31 + i * 7 + lanes); ep[k] = ent[k]; }
+            Strobe8 S; S.from(base.s, lanes);
+            S.meta_ad((const uint8_t *)"rng", 3);
+            S.key_each(ep, 32);
+            std::vector<TranscriptRng> ref;
+            for (int k = 0; k < lanes; k++) { ref.push_back(base); ref.back().finalize(ent[k]); }
+            uint8_t out[8][64], want[64];
+            uint8_t *op[8];
+            for (int k = 0; k < 8; k++) op[k] = out[k];
+            for (int d = 0; d < 300; d++) {
+                S.draw64(op);
+                for (int k = 0; k < lanes; k++) {
+                    ref[k].fill_bytes(want, 64);
+                    if (memcmp(want, out[k], 64)) return 1 + lanes;
+                }
+            }
+        }
+        return 0;
+    }, -1);
+}
+double bpg_rng_rate(uint32_t draws, int lanes) {
+    return guarded([&]() -> double {
+        Transcript T((const uint8_t *)"rate", 4);
+        TranscriptRng base(T);
+        Strobe8 S; S.from(base.s, lanes < 1 ? 1 : (lanes > 8 ? 8 : lanes));
+        uint8_t ent[32] = {1};
+        const uint8_t *ep[8] = {ent, ent, ent, ent, ent, ent, ent, ent};
+        S.meta_ad((const uint8_t *)"rng", 3);
+        S.key_each(ep, 32);
+        std::vector<uint8_t> buf((size_t)8 * 64);
+        uint8_t *op[8];
+        for (int k = 0; k < 8; k++) op[k] = buf.data() + 64 * k;
+        auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t d = 0; d < draws; d++) S.draw64(op);
+        double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return dt > 0 ? draws * (double)S.nstates / dt : 0.0;
+    }, -1.0);
 }
 
 int bpg_last_timings(double *out, int n) {

@@ -109,20 +109,26 @@ struct Workspace {
     int device = 0;
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
-    DBuf sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
+    DBuf wide, sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
         ynwR, pts, okflag;
     PtD *rows_host = nullptr;        // pinned, 8 x 64 rows
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
     dev::ArgStage fold_stage;        // IPP fold kernel arguments
+    hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
+    void sync() {
+        BPG_HIP(hipEventRecord(done_ev, st));
+        BPG_HIP(hipEventSynchronize(done_ev));
+    }
     ~Workspace() {
+        if (done_ev) (void)hipEventDestroy(done_ev);
         if (fold_stage.dev) (void)hipFree(fold_stage.dev);
         if (fold_stage.host) (void)hipHostFree(fold_stage.host);
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
-        DBuf *bufs[] = {&sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
+        DBuf *bufs[] = {&wide, &sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
                         &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
@@ -172,6 +178,7 @@ Workspace &thread_workspace(int device) {
         p.reset(new Workspace());
         p->device = device;
         BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+        BPG_HIP(hipEventCreateWithFlags(&p->done_ev, hipEventBlockingSync | hipEventDisableTiming));
         p->msm.reset(new MsmEngine(p->st));
         BPG_HIP(hipHostMalloc((void **)&p->rows_host, 8 * 64 * sizeof(PtD), hipHostMallocDefault));
         BPG_HIP(hipHostMalloc((void **)&p->small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
@@ -186,7 +193,24 @@ template <class T>
 static T *as(DBuf &b) { return reinterpret_cast<T *>(b.p); }
 
 // ------------------------------------------------------------------ prepare
+std::vector<uint8_t *> PreparedCS::slots(size_t count, size_t bytes) const {
+    std::lock_guard<std::mutex> lk(slot_mu);
+    if (bytes > slot_bytes) {
+        for (uint8_t *b : slot_bufs) (void)hipFree(b);
+        slot_bufs.clear();
+        slot_bytes = bytes;
+    }
+    BPG_HIP(hipSetDevice(device));
+    while (slot_bufs.size() < count) {
+        uint8_t *b = nullptr;
+        BPG_HIP(hipMalloc((void **)&b, slot_bytes));
+        slot_bufs.push_back(b);
+    }
+    return std::vector<uint8_t *>(slot_bufs.begin(), slot_bufs.begin() + count);
+}
+
 PreparedCS::~PreparedCS() {
+    for (uint8_t *b : slot_bufs) (void)hipFree(b);
     DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols};
     for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
 }
@@ -286,7 +310,7 @@ void gpu_pedersen(int device, const std::vector<Scalar> &v, const std::vector<Sc
     uint32_t *outd = reinterpret_cast<uint32_t *>(d + 2 * (size_t)m);
     launch_pedersen(d, d + m, m, ctx.tabB, ctx.tabBb, outd, ws.st);
     BPG_HIP(hipMemcpyAsync(out, outd, (size_t)m * 32, hipMemcpyDeviceToHost, ws.st));
-    BPG_HIP(hipStreamSynchronize(ws.st));
+    ws.sync();
 }
 
 // -------------------------------------------------------------- MSM helpers
@@ -320,7 +344,7 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
     BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, ws.st));
     MsmSeg seg{as<ScD>(ws.small), as<PtD>(ws.pts), n, 0};
     MsmPlan p = ws.msm->enqueue(&seg, 1, 1, ws.rows_host);
-    BPG_HIP(hipStreamSynchronize(ws.st));
+    ws.sync();
     if (!ok) return -1;
     Point r;
     combine_rows(r, ws.rows_host, p.W, p.c);
@@ -352,8 +376,122 @@ static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t cou
 static void check_point_nonidentity(const uint8_t c[32]) { (void)c; }
 
 // ------------------------------------------------------------------- prove
+// Transcript::new(label) + Prover::new + commit(V_i) (prove.rs:45-72 order)
+static Transcript prover_transcript(const PreparedCS &cs, const uint8_t *label, size_t label_len) {
+    Transcript T(label, label_len);
+    T.append_message("dom-sep", (const uint8_t *)"r1cs v1", 7);
+    for (uint32_t i = 0; i < cs.m; i++) T.append_point("V", cs.V.data() + 32 * (size_t)i);
+    T.append_u64("m", cs.m);
+    return T;
+}
+
+// Every TranscriptRng draw of Prover::prove, in program order: i, o, s
+// blindings, s_L[n], s_R[n], then the t_1, t_3..t_6 blindings. The RNG is
+// forked from the transcript before any challenge, so all draws can be made
+// before the device work starts. Up to 8 proofs run in lockstep (Strobe8).
+ProducerStage &producer_stage(int device) {
+    static thread_local std::map<int, std::unique_ptr<ProducerStage>> m;
+    auto &p = m[device];
+    if (!p) {
+        BPG_HIP(hipSetDevice(device));
+        p.reset(new ProducerStage());
+        BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+        for (int b = 0; b < 2; b++) {
+            BPG_HIP(hipHostMalloc((void **)&p->host[b], (size_t)8 * ProducerStage::CHUNK * 64, hipHostMallocDefault));
+            BPG_HIP(hipEventCreateWithFlags(&p->ev[b], hipEventBlockingSync | hipEventDisableTiming));
+            BPG_HIP(hipEventRecord(p->ev[b], p->st));
+        }
+    }
+    BPG_HIP(hipSetDevice(device));
+    return *p;
+}
+ProducerStage::~ProducerStage() {
+    for (int b = 0; b < 2; b++) {
+        if (host[b]) (void)hipHostFree(host[b]);
+        if (ev[b]) (void)hipEventDestroy(ev[b]);
+    }
+    if (st) (void)hipStreamDestroy(st);
+}
+
+void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
+                    int count, RngBlock *const *out, bool dev_out) {
+    if (count < 1 || count > 8) throw std::runtime_error("rng group size");
+    Transcript T = prover_transcript(cs, label, label_len);
+    TranscriptRng base(T);
+    for (uint32_t i = 0; i < cs.m; i++) base.rekey_with_witness_bytes("v_blinding", (const uint8_t *)cs.vb[i].v, 32);
+    Strobe8 S;
+    S.from(base.s, count);
+    S.meta_ad((const uint8_t *)"rng", 3);          // TranscriptRngBuilder::finalize
+    S.key_each(entropy, 32);
+    uint8_t tmp[8][64];
+    uint8_t *tp[8];
+    for (int k = 0; k < 8; k++) tp[k] = tmp[k];
+    auto draw_scalars = [&](Scalar RngBlock::*field) {
+        S.draw64(tp);
+        for (int k = 0; k < count; k++) out[k]->*field = Scalar::from_wide(tmp[k]);
+    };
+    draw_scalars(&RngBlock::i_bl);
+    draw_scalars(&RngBlock::o_bl);
+    draw_scalars(&RngBlock::s_bl);
+    const uint64_t nd = 2 * (uint64_t)cs.n;
+    if (!dev_out) {
+        uint8_t *wp[8];
+        for (uint64_t i = 0; i < nd; i++) {
+            for (int k = 0; k < count; k++) wp[k] = out[k]->wide + 64 * i;
+            for (int k = count; k < 8; k++) wp[k] = tmp[k];
+            S.draw64(wp);
+        }
+    } else {
+        // stream chunks of draws through two pinned staging buffers into
+        // the blocks' device buffers on the caller's stream
+        ProducerStage &ps = producer_stage(cs.device);
+        const uint32_t CH = ProducerStage::CHUNK;
+        uint8_t *wp[8];
+        int buf = 0;
+        for (uint64_t i0 = 0; i0 < nd; i0 += CH, buf ^= 1) {
+            const uint32_t len = (uint32_t)std::min<uint64_t>(CH, nd - i0);
+            BPG_HIP(hipEventSynchronize(ps.ev[buf]));
+            uint8_t *stg = ps.host[buf];
+            for (uint32_t i = 0; i < len; i++) {
+                for (int k = 0; k < 8; k++) wp[k] = stg + ((size_t)k * CH + i) * 64;
+                S.draw64(wp);
+            }
+            for (int k = 0; k < count; k++)
+                BPG_HIP(hipMemcpyAsync(out[k]->wide + 64 * i0, stg + (size_t)k * CH * 64, (size_t)len * 64,
+                                       hipMemcpyHostToDevice, ps.st));
+            BPG_HIP(hipEventRecord(ps.ev[buf], ps.st));
+        }
+        BPG_HIP(hipEventSynchronize(ps.ev[0]));
+        BPG_HIP(hipEventSynchronize(ps.ev[1]));
+    }
+    for (int j = 0; j < 5; j++) {
+        S.draw64(tp);
+        for (int k = 0; k < count; k++) out[k]->tb[j] = Scalar::from_wide(tmp[k]);
+    }
+}
+
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                const uint8_t entropy[32], ProveTimings *tm) {
+    if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
+    Workspace &ws = thread_workspace(cs.device);
+    double t0 = now_ms();
+    ws.stage(2 * (size_t)cs.n * 64 + 64);
+    RngBlock rb;
+    rb.wide = ws.s_host;
+    RngBlock *rbp = &rb;
+    rng_draw_group(cs, label, label_len, &entropy, 1, &rbp, false);
+    double t1 = now_ms();
+    ProveTimings t;
+    std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, rb, &t);
+    t.rng_ms = t1 - t0;
+    t.total_ms += t1 - t0;
+    last_timings() = t;
+    if (tm) *tm = t;
+    return pr;
+}
+
+std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
+                                   ProveTimings *tm) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t n = cs.n, m = cs.m, N = cs.N, lgN = cs.lgN;
@@ -362,16 +500,8 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     hipStream_t st = ws.st;
     double t0 = now_ms();
     ws.tabs.grow(8 * 40 * sizeof(ScD));
-
-    // transcript prefix: Transcript::new(label) + Prover::new + commit(V_i)
-    Transcript T(label, label_len);
-    T.append_message("dom-sep", (const uint8_t *)"r1cs v1", 7);
-    for (uint32_t i = 0; i < m; i++) T.append_point("V", cs.V.data() + 32 * (size_t)i);
-    T.append_u64("m", m);
-    TranscriptRng rng(T);
-    for (uint32_t i = 0; i < m; i++) rng.rekey_with_witness_bytes("v_blinding", (const uint8_t *)cs.vb[i].v, 32);
-    rng.finalize(entropy);
-    Scalar i_bl = rng.random_scalar(), o_bl = rng.random_scalar(), s_bl = rng.random_scalar();
+    Transcript T = prover_transcript(cs, label, label_len);
+    const Scalar i_bl = rb.i_bl, o_bl = rb.o_bl, s_bl = rb.s_bl;
 
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G> (blinding terms added on the host)
     PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
@@ -384,23 +514,24 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         pA = ws.msm->enqueue(segA, 3, 2, rowsA);
         ws.prof_end(ph);
     }
-    // s_L, s_R: 2n serial TranscriptRng draws (one Keccak-f each) overlap the MSM
-    double t_rng0 = now_ms();
-    ws.stage(2 * (size_t)n * 32 + 64);
-    ScD *sh = reinterpret_cast<ScD *>(ws.s_host);
-    for (uint32_t i = 0; i < 2 * n; i++) sh[i] = to_dev(rng.random_scalar());
-    double t_rng1 = now_ms();
+    // s_L | s_R: raw 64-byte draws -> device, reduced mod l there
     ws.sL.grow((size_t)n * sizeof(ScD) + 64);
     ws.sR.grow((size_t)n * sizeof(ScD) + 64);
+    ws.wide.grow(2 * (size_t)n * 64 + 64);
     if (n) {
-        BPG_HIP(hipMemcpyAsync(ws.sL.p, sh, (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, st));
-        BPG_HIP(hipMemcpyAsync(ws.sR.p, sh + n, (size_t)n * sizeof(ScD), hipMemcpyHostToDevice, st));
+        const uint8_t *wd = rb.wide;
+        if (!rb.on_device) {
+            BPG_HIP(hipMemcpyAsync(ws.wide.p, rb.wide, 2 * (size_t)n * 64, hipMemcpyHostToDevice, st));
+            wd = as<uint8_t>(ws.wide);
+        }
+        launch_wide_reduce(wd, n, as<ScD>(ws.sL), st);
+        launch_wide_reduce(wd + 64 * (size_t)n, n, as<ScD>(ws.sR), st);
         MsmSeg segS[2] = {{as<ScD>(ws.sL), ctx.G, n, 0}, {as<ScD>(ws.sR), ctx.H, n, 0}};
         int ph = ws.prof_begin("msm_commit", 2.0 * n * (64 + 32));
         pS = ws.msm->enqueue(segS, 2, 1, rowsS);
         ws.prof_end(ph);
     }
-    BPG_HIP(hipStreamSynchronize(st));
+    ws.sync();
     Point AI, AO, S, tmp;
     if (n) {
         combine_rows(AI, rowsA, pA.W, pA.c);
@@ -437,7 +568,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         DBuf lo2, hi2;
         pow_vector(ws, 2, y_inv, N, lo2, hi2, as<ScD>(ws.yipm));
         pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);   // also syncs tables below
-        BPG_HIP(hipStreamSynchronize(st));
+        ws.sync();
         if (lo2.p) (void)hipFree(lo2.p);
         if (hi2.p) (void)hipFree(hi2.p);
     }
@@ -469,12 +600,11 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(ws.partial), dsmall + 6, st);
     else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
-    BPG_HIP(hipStreamSynchronize(st));
+    ws.sync();
     Scalar tp[6];
     for (int k = 0; k < 6; k++) tp[k] = from_dev(ws.small_host[1000 + k]);
     Scalar tb2 = from_dev(ws.small_host[1006]);
-    Scalar tb1 = rng.random_scalar(), tb3 = rng.random_scalar(), tb4 = rng.random_scalar(), tb5 = rng.random_scalar(),
-           tb6 = rng.random_scalar();
+    const Scalar tb1 = rb.tb[0], tb3 = rb.tb[1], tb4 = rb.tb[2], tb5 = rb.tb[3], tb6 = rb.tb[4];
     uint8_t cT[5][32];
     pedersen_commit(cT[0], tp[0], tb1);
     pedersen_commit(cT[1], tp[2], tb3);
@@ -535,7 +665,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         int ph = ws.prof_begin("msm_ipp", (4.0 * h + 2) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, 6, 2, rowsLR);
         ws.prof_end(ph);
-        BPG_HIP(hipStreamSynchronize(st));
+        ws.sync();
         Point Lp, Rp;
         combine_rows(Lp, rowsLR, pl.W, pl.c);
         combine_rows(Rp, rowsLR + pl.W, pl.W, pl.c);
@@ -563,7 +693,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     }
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1010, ws.a.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1011, ws.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
-    BPG_HIP(hipStreamSynchronize(st));
+    ws.sync();
     Scalar fa = from_dev(ws.small_host[1010]), fb = from_dev(ws.small_host[1011]);
     ws.prof_flush();
     double t3 = now_ms();
@@ -583,7 +713,6 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     fa.to_bytes(b32); put(b32);
     fb.to_bytes(b32); put(b32);
     ProveTimings t;
-    t.rng_ms = t_rng1 - t_rng0;
     t.commit_ms = t1 - t0;
     t.vec_ms = t2 - t1;
     t.ipp_ms = t3 - t2;
@@ -653,7 +782,7 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
         DBuf lo2, hi2;
         pow_vector(ws, 2, y_inv, N, lo2, hi2, as<ScD>(ws.yipm));
         pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);
-        BPG_HIP(hipStreamSynchronize(st));
+        ws.sync();
         if (lo2.p) (void)hipFree(lo2.p);
         if (hi2.p) (void)hipFree(hi2.p);
     }
@@ -727,7 +856,7 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
     launch_decompress(compd, as<PtD>(ws.pts), as<int>(ws.okflag), ns, st);
     int ok = 0;
     BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, st));
-    BPG_HIP(hipStreamSynchronize(st));
+    ws.sync();
     if (!ok) return 0;
     Scalar delta = from_dev(hsm[0]);
     Scalar wc = from_dev(wvh[m]);
@@ -740,7 +869,7 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
     BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
     MsmSeg seg[3] = {{as<ScD>(ws.gh), ctx.G, N, 0}, {as<ScD>(ws.gh) + N, ctx.H, N, 0}, {sscal, as<PtD>(ws.pts), ns, 0}};
     MsmPlan pl = ws.msm->enqueue(seg, 3, 1, ws.rows_host);
-    BPG_HIP(hipStreamSynchronize(st));
+    ws.sync();
     Point R;
     combine_rows(R, ws.rows_host, pl.W, pl.c);
     // B and B_blinding terms

@@ -12,6 +12,7 @@
 #include "../../../include/bpg.h"
 #include "../device/kernels.h"
 #include "hcrypto.h"
+#include "rng8.h"
 
 namespace bpg {
 
@@ -44,6 +45,11 @@ struct PreparedCS {
     DBuf col_ptr, col_row, col_coeff, short_cols, long_cols;
     uint32_t nshort = 0, nlong = 0, ncol = 0;
     std::vector<uint32_t> huge_cols, col_ptr_host;
+    // pinned host buffers for batched RNG output (grow-only, reused)
+    mutable std::mutex slot_mu;
+    mutable std::vector<uint8_t *> slot_bufs;
+    mutable size_t slot_bytes = 0;
+    std::vector<uint8_t *> slots(size_t count, size_t bytes) const;
     ~PreparedCS();
 };
 
@@ -56,9 +62,32 @@ Workspace &thread_workspace(int device);
 
 struct ProveTimings { double rng_ms = 0, commit_ms = 0, vec_ms = 0, ipp_ms = 0, total_ms = 0; };
 
+// All TranscriptRng draws of one proof (Prover::prove order).
+struct RngBlock {
+    Scalar i_bl, o_bl, s_bl;
+    Scalar tb[5];                // t_1, t_3, t_4, t_5, t_6 blindings
+    uint8_t *wide = nullptr;     // 2n x 64 raw bytes: s_L then s_R
+    bool on_device = false;      // wide is a device buffer (batched path)
+};
+// Per-thread staging of RNG output into device buffers.
+struct ProducerStage {
+    static const uint32_t CHUNK = 2048;   // draws per staged chunk
+    hipStream_t st = nullptr;
+    uint8_t *host[2] = {nullptr, nullptr};   // pinned, 8 x CHUNK x 64 B each
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    ~ProducerStage();
+};
+ProducerStage &producer_stage(int device);
+// Draw the RNG streams of `count` (<= 8) proofs of `cs` in lockstep. With
+// dev_out the s_L | s_R draws go to out[k]->wide as device buffers.
+void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
+                    int count, RngBlock *const *out, bool dev_out);
 // Prover::prove. Returns proof bytes (R1CSProof::to_bytes, one-phase layout).
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                const uint8_t entropy[32], ProveTimings *tm = nullptr);
+// Prover::prove after the RNG phase (the device part and the transcript).
+std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
+                                   ProveTimings *tm = nullptr);
 // Verifier::verify; returns 1 accept / 0 reject.
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                const uint8_t *proof, size_t proof_len, const uint8_t entropy[32]);

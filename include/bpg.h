@@ -207,6 +207,13 @@ int bpg_kernel_stats(const char *name, uint64_t *launches, double *total_ms,
                      double *alg_bytes);
 void bpg_kernel_stats_reset(void);
 
+/* Diagnostics for the batched RNG (lockstep STROBE / TranscriptRng for up
+ * to 8 proofs, AVX-512 when available): self-test against the scalar
+ * TranscriptRng (0 = identical output), and draws per second of one thread
+ * driving `lanes` proofs. */
+int bpg_rng_selftest(void);
+double bpg_rng_rate(uint32_t draws, int lanes);
+
 #ifdef __cplusplus
 }
 #endif
