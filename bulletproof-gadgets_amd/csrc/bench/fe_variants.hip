@@ -12,6 +12,40 @@
 #include <stdint.h>
 #include "../device/dev_field.h"
 
+// 8 x 32-bit limbs, fold 2^256 == 38 (the layout used before the radix-2^25.5 switch)
+struct fe8 { uint32_t v[8]; };
+DEVI void fe8_reduce16(fe8 &r, const uint32_t t[16]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) { c += (uint64_t)t[8 + i] * 38u + t[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+    c *= 38;
+#pragma unroll
+    for (int i = 0; i < 8; i++) { c += r.v[i]; r.v[i] = (uint32_t)c; c >>= 32; }
+    r.v[0] += (uint32_t)c * 38;
+}
+DEVI void fe8_mul(fe8 &r, const fe8 &a, const fe8 &b) {
+    uint32_t t[16];
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) { c += (uint64_t)a.v[0] * b.v[j]; t[j] = (uint32_t)c; c >>= 32; }
+    t[8] = (uint32_t)c;
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+        c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) { c += (uint64_t)a.v[i] * b.v[j] + t[i + j]; t[i + j] = (uint32_t)c; c >>= 32; }
+        t[i + 8] = (uint32_t)c;
+    }
+    fe8_reduce16(r, t);
+}
+DEVI void fe8_canon(fe8 &r, const fe8 &a) {
+    // value < 2^256 -> canonical via the 10-limb path
+    fe x = fe_from_words(a.v[0], a.v[1], a.v[2], a.v[3], a.v[4], a.v[5], a.v[6], a.v[7] & 0x7fffffffu);
+    x.v[0] += 19 * (a.v[7] >> 31);
+    uint32_t w[8]; fe_tow(w, x);
+    for (int i = 0; i < 8; i++) r.v[i] = w[i];
+}
+
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
 DEVI void mad_cy(uint64_t &acc, uint32_t &hi, uint32_t a, uint32_t b) {
@@ -20,7 +54,7 @@ DEVI void mad_cy(uint64_t &acc, uint32_t &hi, uint32_t a, uint32_t b) {
     asm volatile("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(hi), "=s"(cy) : "s"(cy));
 }
 
-DEVI void fe_mul_v1(fe &r, const fe &a, const fe &b) {
+DEVI void fe_mul_v1(fe8 &r, const fe8 &a, const fe8 &b) {
     uint32_t t[16];
     uint64_t acc = 0;
     uint32_t hi = 0;
@@ -37,13 +71,13 @@ DEVI void fe_mul_v1(fe &r, const fe &a, const fe &b) {
         hi = 0;
     }
     t[15] = (uint32_t)acc;
-    fe_reduce16(r, t);
+    fe8_reduce16(r, t);
 }
 
 // ---- V2: radix 2^25.5, limbs alternately 26 and 25 bits
 struct f10 { uint32_t v[10]; };
-DEVI void f10_from(f10 &r, const fe &a) {
-    fe c; fe_canon(c, a);
+DEVI void f10_from(f10 &r, const fe8 &a) {
+    fe8 c; fe8_canon(c, a);
     // unpack 255 bits into 26,25,26,25,...
     uint32_t w[8]; for (int i = 0; i < 8; i++) w[i] = c.v[i];
     int pos = 0;
@@ -57,7 +91,7 @@ DEVI void f10_from(f10 &r, const fe &a) {
         pos += bits;
     }
 }
-DEVI void f10_to(fe &r, const f10 &a) {
+DEVI void f10_to(fe8 &r, const f10 &a) {
     // value = sum a_i 2^{ceil(25.5 i)}; limbs may exceed their width slightly
     uint32_t w[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int pos = 0;
@@ -123,7 +157,7 @@ DEVI void f10_mul(f10 &h, const f10 &f, const f10 &g) {
     h.v[5] = (uint32_t)h5; h.v[6] = (uint32_t)h6; h.v[7] = (uint32_t)h7; h.v[8] = (uint32_t)h8; h.v[9] = (uint32_t)h9;
 }
 
-__device__ void seed_fe(fe &x, uint32_t s) {
+__device__ void seed_fe(fe8 &x, uint32_t s) {
     for (int i = 0; i < 8; i++) { s = s * 1664525u + 1013904223u; x.v[i] = s; }
     x.v[7] &= 0x7fffffff;
 }
@@ -131,7 +165,7 @@ __device__ void seed_fe(fe &x, uint32_t s) {
 template <int V>
 __global__ __launch_bounds__(256) void k_chain(uint32_t *out, int iters) {
     uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    fe x0, x1, y;
+    fe8 x0, x1, y;
     seed_fe(x0, tid * 3 + 1); seed_fe(x1, tid * 3 + 2); seed_fe(y, 99);
     if (V == 2) {
         f10 a, b, g;
@@ -140,22 +174,27 @@ __global__ __launch_bounds__(256) void k_chain(uint32_t *out, int iters) {
         f10_to(x0, a); f10_to(x1, b);
     } else {
         for (int i = 0; i < iters; i++) {
-            if (V == 0) { fe_mul(x0, x0, y); fe_mul(x1, x1, y); }
+            if (V == 0) { fe8_mul(x0, x0, y); fe8_mul(x1, x1, y); }
             else { fe_mul_v1(x0, x0, y); fe_mul_v1(x1, x1, y); }
         }
     }
-    fe c0, c1; fe_canon(c0, x0); fe_canon(c1, x1);
+    fe8 c0, c1; fe8_canon(c0, x0); fe8_canon(c1, x1);
     uint32_t h = 0;
     for (int i = 0; i < 8; i++) h = h * 31 + c0.v[i] + 7 * c1.v[i];
     out[tid] = h;
 }
+// production radix-2^25.5 square (dev_field.h fe_sq)
 template <int V>
 __global__ __launch_bounds__(256) void k_sqchain(uint32_t *out, int iters) {
     uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    fe x0, x1;
-    seed_fe(x0, tid * 3 + 1); seed_fe(x1, tid * 3 + 2);
+    fe8 s0, s1;
+    seed_fe(s0, tid * 3 + 1); seed_fe(s1, tid * 3 + 2);
+    fe x0 = fe_from_words(s0.v[0], s0.v[1], s0.v[2], s0.v[3], s0.v[4], s0.v[5], s0.v[6], s0.v[7]);
+    fe x1 = fe_from_words(s1.v[0], s1.v[1], s1.v[2], s1.v[3], s1.v[4], s1.v[5], s1.v[6], s1.v[7]);
     for (int i = 0; i < iters; i++) { fe_sq(x0, x0); fe_sq(x1, x1); }
-    fe c0, c1; fe_canon(c0, x0); fe_canon(c1, x1);
+    uint32_t w0[8], w1[8]; fe_tow(w0, x0); fe_tow(w1, x1);
+    fe8 c0, c1;
+    for (int i = 0; i < 8; i++) { c0.v[i] = w0[i]; c1.v[i] = w1[i]; }
     uint32_t h = 0;
     for (int i = 0; i < 8; i++) h = h * 31 + c0.v[i] + 7 * c1.v[i];
     out[tid] = h;
@@ -175,7 +214,7 @@ int main() {
     CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     typedef void (*kf)(uint32_t *, int);
     kf ks[4] = {k_chain<0>, k_chain<1>, k_chain<2>, k_sqchain<0>};
-    const char *nm[4] = {"V0 fe_mul (current)", "V1 comba+carry asm", "V2 10x25.5 carry-free", "fe_sq (current)"};
+    const char *nm[4] = {"V0 8x32 schoolbook", "V1 comba+carry asm", "V2 10x25.5 carry-free", "fe_sq (10x25.5)"};
     for (int v = 0; v < 4; v++) {
         hipLaunchKernelGGL(ks[v], dim3(blocks), dim3(threads), 0, 0, d + v * nt, iters);
         CHK(hipDeviceSynchronize());

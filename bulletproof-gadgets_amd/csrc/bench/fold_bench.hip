@@ -2,6 +2,8 @@
 // and one MSM job at the config-5 round-0 size, for occupancy/variant
 // experiments. Points come from the generator map on random bytes.
 #include "../device/kernels.hip"
+#include "../host/hcrypto.h"
+#include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
@@ -25,15 +27,48 @@ int main(int argc, char **argv) {
     ArgStage stage;
     hipStream_t st; BPG_HIP(hipStreamCreate(&st));
     hipEvent_t e0, e1; BPG_HIP(hipEventCreate(&e0)); BPG_HIP(hipEventCreate(&e1));
-    launch_ipp_fold_points(G, H, h, n, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
-    BPG_HIP(hipStreamSynchronize(st));
     const int reps = 3;
-    BPG_HIP(hipEventRecord(e0, st));
-    for (int k = 0; k < reps; k++) launch_ipp_fold_points(G, H, h, n, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
-    BPG_HIP(hipEventRecord(e1, st));
-    BPG_HIP(hipEventSynchronize(e1));
-    float ms; BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
-    printf("fold h=%u (2h=%u lanes): %.3f ms per launch, %.1f ns per lane\n", h, 2 * h, ms / reps, ms / reps * 1e6 / (2.0 * h));
+    float ms;
+    std::vector<uint32_t> cin((size_t)4 * h * 8), cout_((size_t)2 * h * 8);
+    uint32_t *dcin, *dcout;
+    BPG_HIP(hipMalloc(&dcin, cin.size() * 4)); BPG_HIP(hipMalloc(&dcout, cout_.size() * 4));
+    launch_compress(G, dcin, 2 * h, st); launch_compress(H, dcin + (size_t)16 * h, 2 * h, st);
+    BPG_HIP(hipMemcpyAsync(cin.data(), dcin, cin.size() * 4, hipMemcpyDeviceToHost, st));
+    BPG_HIP(hipStreamSynchronize(st));
+    uint32_t ns[4] = {n, 744712, h, 2 * h};
+    for (uint32_t nn : ns) {
+        launch_ipp_fold_points(G, H, h, nn, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
+        BPG_HIP(hipStreamSynchronize(st));
+        BPG_HIP(hipEventRecord(e0, st));
+        for (int k = 0; k < reps; k++) launch_ipp_fold_points(G, H, h, nn, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
+        BPG_HIP(hipEventRecord(e1, st));
+        BPG_HIP(hipEventSynchronize(e1));
+        BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
+        // check sampled lanes against host arithmetic
+        launch_compress(Go, dcout, h, st); launch_compress(Ho, dcout + (size_t)8 * h, h, st);
+        BPG_HIP(hipMemcpyAsync(cout_.data(), dcout, cout_.size() * 4, hipMemcpyDeviceToHost, st));
+        BPG_HIP(hipStreamSynchronize(st));
+        int bad = 0, checked = 0;
+        const uint32_t a = nn > h ? std::min(nn - h, h) : 0, bnd = std::min(nn, h);
+        uint32_t lanes[] = {0, 1, 63, 64, a ? a - 1 : 0, a, a + 1, bnd ? bnd - 1 : 0, bnd < h ? bnd : 0, h - 1, h / 3};
+        for (int v = 0; v < 2; v++)
+            for (uint32_t i : lanes) {
+                if (i >= h) continue;
+                bool special = i >= a && i < bnd;
+                const ScD &rho = r[2 * v + (special ? 1 : 0)];
+                bpg::Point PL, PR, t, want;
+                const uint8_t *pl = (const uint8_t *)&cin[((size_t)v * 2 * h + i) * 8];
+                const uint8_t *pr = (const uint8_t *)&cin[((size_t)v * 2 * h + h + i) * 8];
+                bpg::ristretto_decompress(PL, pl); bpg::ristretto_decompress(PR, pr);
+                bpg::Scalar sr; memcpy(sr.v, rho.v, 32);
+                bpg::mul_var(t, sr, PR); bpg::pt_add(want, PL, t);
+                uint8_t wb[32]; bpg::ristretto_compress(wb, want);
+                checked++;
+                if (memcmp(wb, &cout_[((size_t)v * h + i) * 8], 32)) bad++;
+            }
+        printf("fold h=%u n=%u: %.3f ms per launch (%.2f ns/lane); check %d/%d lanes bad\n", h, nn, ms / reps,
+               ms / reps * 1e6 / (2.0 * h), bad, checked);
+    }
     // one MSM job: 4 segments of h points (round-0 L/R shape)
     std::vector<ScD> sc((size_t)4 * h);
     for (auto &s : sc) { for (int i = 0; i < 8; i++) s.v[i] = rand() * 2654435761u + rand(); s.v[7] &= 0x0fffffff; }

@@ -126,7 +126,7 @@ void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStr
 // Kernel-argument block staged through pinned host memory to a device buffer
 // (one per stream; the host side is rewritten only after the stream has
 // passed the previous use).
-struct ArgStage { void *dev = nullptr, *host = nullptr; };
+struct ArgStage { void *dev = nullptr, *host = nullptr; hipEvent_t copied = nullptr; };
 void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
                             ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage, hipStream_t st);
 // verifier helpers

@@ -335,62 +335,88 @@ __global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ k
     ge_store(buckets + k, acc);
     bflag[k] = 1;
 }
-// r = k * p for small k (weights of bucket segments)
-DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {
-    ge_identity(r);
-    if (!k) return;
-    int top = 31 - __clz(k);
-    r = p;
-    for (int b = top - 1; b >= 0; b--) {
-        ge_dbl(r, r);
-        if ((k >> b) & 1) ge_add(r, r, p);
-    }
-}
-DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict__ F, uint32_t i) {
+// Window rows from buckets: R_row = sum_b (b+1) S_b over the half buckets.
+// Level 1 (thread per segment of L buckets): A_s = sum_j (j+1) S_{sL+j} and
+// T_s = sum_j S_{sL+j} by the backward running sum (2L additions, no
+// per-thread scalar multiple). Then R = sum_s A_s + L * sum_s s T_s.
+DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict__ F, size_t i) {
     if (F[i]) ge_load(p, B + i); else ge_identity(p);
 }
-// sum_{b in seg} (b+1) * S_b = acc + lo * run, with acc weights 1..seglen
 __global__ __launch_bounds__(64) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
                                                    uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
-                                                   ge *__restrict__ segacc) {
+                                                   ge *__restrict__ segA, ge *__restrict__ segT) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= rows * nseg) return;
-    uint32_t row = t / nseg, s = t % nseg;
-    uint32_t lo = s * seglen;
-    const size_t b0 = (size_t)row * half + lo;
+    uint32_t row = t / nseg, sgi = t % nseg;
+    const size_t b0 = (size_t)row * half + (size_t)sgi * seglen;
     ge run, acc, p;
-    bucket_load(run, buckets + b0, bflag + b0, seglen - 1);
+    bucket_load(run, buckets, bflag, b0 + seglen - 1);
     acc = run;
     for (int b = (int)seglen - 2; b >= 0; b--) {
-        bucket_load(p, buckets + b0, bflag + b0, b);
+        bucket_load(p, buckets, bflag, b0 + b);
         ge_add(run, run, p);
         ge_add(acc, acc, run);
     }
-    if (lo) {
-        ge_mul_small(p, run, lo);
-        ge_add(acc, acc, p);
-    }
-    ge_store(segacc + t, acc);
+    ge_store(segA + t, acc);
+    ge_store(segT + t, run);
 }
-__global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segacc, uint32_t nseg,
-                                                    ge *__restrict__ rows_out) {
+DEVI void ge_dbl_n(ge &r, int n) {
+    for (int i = 1; i < n; i++) ge_dbl_t<false>(r, r);
+    if (n > 0) ge_dbl_t<true>(r, r);
+}
+// Level 2, one block per row. Thread t owns segments [tK, tK+K):
+//   sum_s s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t,
+//   sum_t t run_t = sum_{k>=1} suffix_k (suffix scan in LDS).
+// Each thread forms Q_t = A'_t + L * ((acc_t - run_t) + K * [t>=1] suffix_t);
+// a tree reduction of Q_t gives R. L and K are powers of two.
+__global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
+                                                    uint32_t nseg, int lgL, ge *__restrict__ rows_out) {
     __shared__ ge sh[256];
-    uint32_t row = blockIdx.x, tid = threadIdx.x;
-    const ge *S = segacc + (size_t)row * nseg;
-    ge acc, p;
-    ge_identity(acc);
-    for (uint32_t s = tid; s < nseg; s += 256) { ge_load(p, S + s); ge_add(acc, acc, p); }
-    ge_store(&sh[tid], acc);
+    const uint32_t row = blockIdx.x, t = threadIdx.x;
+    const uint32_t K = (nseg + 255) / 256;
+    int lgK = 0;
+    while ((1u << lgK) < K) lgK++;
+    const ge *A = segA + (size_t)row * nseg, *T = segT + (size_t)row * nseg;
+    ge sumA, run, acc, p;
+    ge_identity(sumA); ge_identity(run); ge_identity(acc);
+    for (int j = (int)K - 1; j >= 0; j--) {
+        uint32_t s = t * K + j;
+        if (s >= nseg) continue;
+        ge_load(p, A + s); ge_add(sumA, sumA, p);
+        ge_load(p, T + s); ge_add(run, run, p);
+        ge_add(acc, acc, run);
+    }
+    // inclusive suffix scan of run over threads
+    ge_store(&sh[t], run);
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        __syncthreads();
+        ge a, b;
+        const bool act = t + d < 256;
+        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
+        __syncthreads();
+        if (act) ge_store(&sh[t], a);
+    }
+    __syncthreads();
+    ge q, suf;
+    ge_load(suf, &sh[t]);
+    if (t == 0) ge_identity(suf);
+    ge_dbl_n(suf, lgK);                    // K * suffix_t
+    ge_sub(q, acc, run);
+    ge_add(q, q, suf);
+    ge_dbl_n(q, lgL);                      // L * (...)
+    ge_add(q, q, sumA);
+    __syncthreads();
+    ge_store(&sh[t], q);
     for (int w = 128; w >= 1; w >>= 1) {
         __syncthreads();
-        if (tid < (uint32_t)w) {
+        if (t < (uint32_t)w) {
             ge a, b;
-            ge_load(a, &sh[tid]); ge_load(b, &sh[tid + w]);
+            ge_load(a, &sh[t]); ge_load(b, &sh[t + w]);
             ge_add(a, a, b);
-            ge_store(&sh[tid], a);
+            ge_store(&sh[t], a);
         }
     }
-    if (tid == 0) { ge r; ge_load(r, &sh[0]); ge_store(rows_out + row, r); }
+    if (t == 0) { ge r; ge_load(r, &sh[0]); ge_store(rows_out + row, r); }
 }
 
 static int msm_window(uint64_t total) {
@@ -430,7 +456,7 @@ void MsmEngine::reserve(const MsmPlan &p) {
     rp_a_.grow(p.capE * sizeof(ge)); rp_b_.grow(p.capE * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
     bflag_.grow((size_t)p.rows * p.half);
-    segacc_.grow((size_t)p.rows * p.nseg_per_row * sizeof(ge));
+    segacc_.grow((size_t)2 * p.rows * p.nseg_per_row * sizeof(ge));
     rows_dev_.grow((size_t)p.rows * sizeof(ge));
 }
 
@@ -464,7 +490,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     // passes: enough that T^passes exceeds the largest possible run (total)
     p.passes = 1;
     { uint64_t r = RBK_T / 2; while (r < total + 1) { r *= RBK_T / 2; p.passes++; } }
-    p.seglen = p.half < 16 ? p.half : 16;
+    p.seglen = p.half < 8 ? p.half : 8;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
         for (int r = 0; r < p.rows; r++) {
@@ -525,11 +551,13 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     }
     hipLaunchKernelGGL(k_rbk_final, dim3(nblk(Ebound, 64)), dim3(64), 0, st_, kin, pin, Ein, Ebound, buckets, bflag);
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
+    ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
     hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
-                       (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row,
-                       AS_GE(segacc_.p));
-    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, AS_CGE(segacc_.p), (uint32_t)p.nseg_per_row,
-                       AS_GE(rows_dev_.p));
+                       (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, segA, segT);
+    int lgL = 0;
+    while ((1 << lgL) < p.seglen) lgL++;
+    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
+                       (uint32_t)p.nseg_per_row, lgL, AS_GE(rows_dev_.p));
     BPG_HIP(hipGetLastError());
     BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;
@@ -979,6 +1007,9 @@ void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t
     if (!stage.dev) {
         BPG_HIP(hipMalloc(&stage.dev, sizeof(FoldArgs)));
         BPG_HIP(hipHostMalloc(&stage.host, sizeof(FoldArgs), hipHostMallocDefault));
+        BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
+    } else {
+        BPG_HIP(hipEventSynchronize(stage.copied));   // previous upload has left the host buffer
     }
     FoldArgs &A = *reinterpret_cast<FoldArgs *>(stage.host);
     A = FoldArgs{};
@@ -1003,6 +1034,7 @@ void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t
     A.blk0[A.nseg] = blocks;
     if (!blocks) return;
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldArgs), hipMemcpyHostToDevice, st));
+    BPG_HIP(hipEventRecord(stage.copied, st));
     hipLaunchKernelGGL(k_ipp_fold_points, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }

@@ -125,6 +125,7 @@ struct Workspace {
         if (done_ev) (void)hipEventDestroy(done_ev);
         if (fold_stage.dev) (void)hipFree(fold_stage.dev);
         if (fold_stage.host) (void)hipHostFree(fold_stage.host);
+        if (fold_stage.copied) (void)hipEventDestroy(fold_stage.copied);
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
