@@ -25,7 +25,7 @@ EXPORTS = [
     "bpg_prove_batch", "bpg_last_timings", "bpg_msm", "bpg_synthesize", "bpg_synthesize_verifier",
     "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free", "bpg_mimc_hash",
     "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
-    "bpg_rng_rate",
+    "bpg_rng_rate", "bpg_set_fold_tables",
 ]
 
 

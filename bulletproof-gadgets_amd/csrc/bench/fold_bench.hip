@@ -14,10 +14,10 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> uni((size_t)2 * h * 64);
     srand(1);
     for (auto &b : uni) b = rand() & 255;
-    uint8_t *duni; PtD *G, *H, *Go, *Ho;
+    uint8_t *duni; NielsD *G, *H; PtD *Go, *Ho;
     BPG_HIP(hipMalloc(&duni, uni.size()));
     BPG_HIP(hipMemcpy(duni, uni.data(), uni.size(), hipMemcpyHostToDevice));
-    BPG_HIP(hipMalloc(&G, (size_t)2 * h * sizeof(PtD))); BPG_HIP(hipMalloc(&H, (size_t)2 * h * sizeof(PtD)));
+    BPG_HIP(hipMalloc(&G, (size_t)2 * h * sizeof(NielsD))); BPG_HIP(hipMalloc(&H, (size_t)2 * h * sizeof(NielsD)));
     BPG_HIP(hipMalloc(&Go, (size_t)h * sizeof(PtD))); BPG_HIP(hipMalloc(&Ho, (size_t)h * sizeof(PtD)));
     launch_gens_map(duni, G, 2 * h, 0);
     launch_gens_map(duni, H, 2 * h, 0);
@@ -37,10 +37,10 @@ int main(int argc, char **argv) {
     BPG_HIP(hipStreamSynchronize(st));
     uint32_t ns[4] = {n, 744712, h, 2 * h};
     for (uint32_t nn : ns) {
-        launch_ipp_fold_points(G, H, h, nn, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
+        launch_ipp_fold_points(G, H, MSM_NIELS, h, nn, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
         BPG_HIP(hipStreamSynchronize(st));
         BPG_HIP(hipEventRecord(e0, st));
-        for (int k = 0; k < reps; k++) launch_ipp_fold_points(G, H, h, nn, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
+        for (int k = 0; k < reps; k++) launch_ipp_fold_points(G, H, MSM_NIELS, h, nn, r[0], r[1], r[2], r[3], Go, Ho, stage, st);
         BPG_HIP(hipEventRecord(e1, st));
         BPG_HIP(hipEventSynchronize(e1));
         BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
@@ -77,10 +77,10 @@ int main(int argc, char **argv) {
     MsmEngine eng(st);
     PtD *rows; BPG_HIP(hipHostMalloc((void **)&rows, 128 * sizeof(PtD), hipHostMallocDefault));
     MsmSeg seg[4] = {{dsc, G + h, h, 0}, {dsc + h, H, h, 0}, {dsc + 2 * (size_t)h, G, h, 1}, {dsc + 3 * (size_t)h, H + h, h, 1}};
-    eng.enqueue(seg, 4, 2, rows);
+    eng.enqueue(seg, 4, 2, rows, MSM_NIELS);
     BPG_HIP(hipStreamSynchronize(st));
     BPG_HIP(hipEventRecord(e0, st));
-    for (int k = 0; k < reps; k++) eng.enqueue(seg, 4, 2, rows);
+    for (int k = 0; k < reps; k++) eng.enqueue(seg, 4, 2, rows, MSM_NIELS);
     BPG_HIP(hipEventRecord(e1, st));
     BPG_HIP(hipEventSynchronize(e1));
     BPG_HIP(hipEventElapsedTime(&ms, e0, e1));

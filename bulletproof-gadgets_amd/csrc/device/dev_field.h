@@ -44,6 +44,9 @@ struct fe { uint32_t v[10]; };
 struct sc { uint32_t v[8]; };
 struct ge { fe X, Y, Z, T; };           // extended twisted Edwards, a = -1
 struct gec { fe YpX, YmX, Z2, T2d; };   // cached: (Y+X, Y-X, 2Z, 2dT)
+// affine Niels (Z = 1): (y+x, y-x, 2dxy), padded to 128 B so a random gather
+// is exactly one 128-B line (generators, decompressed inputs)
+struct gen { fe YpX, YmX, T2d; uint32_t pad[2]; };
 
 #define FE_M26 0x3ffffffu
 #define FE_M25 0x1ffffffu
@@ -456,6 +459,36 @@ DEVI void ge_sub_c(ge &r, const ge &p, const gec &q) {
     fe_add_nc(h, b, a);
     fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
 }
+// madd-2008-hwcd-3 (a = -1) with an affine Niels right operand: 7M.
+// D = 2 Z1 unreduced (2T): F = D - C <= 4T, G = D + C <= 3T, E <= 3T,
+// H <= 2T, so every product below keeps fe_mul's argument bounds.
+DEVI void ge_madd(ge &r, const ge &p, const gen &q) {
+    fe a, b, c, d, e, f, g, h;
+    fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q.YmX);
+    fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q.YpX);
+    fe_mul(c, p.T, q.T2d);
+    fe_add_nc(d, p.Z, p.Z);
+    fe_sub_nc(e, b, a);
+    fe_sub_nc(f, d, c);
+    fe_add_nc(g, d, c);
+    fe_add_nc(h, b, a);
+    fe_mul(r.X, f, e); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+}
+DEVI void gen_cneg(gen &c, bool neg) {
+    if (neg) { fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; fe_neg(c.T2d, c.T2d); }
+}
+DEVI void gen_identity(gen &c) { fe_one(c.YpX); fe_one(c.YmX); fe_zero(c.T2d); c.pad[0] = c.pad[1] = 0; }
+// affine Niels as a cached point (2Z = 2)
+DEVI void gen_to_cached(gec &r, const gen &q) { r.YpX = q.YpX; r.YmX = q.YmX; fe_zero(r.Z2); r.Z2.v[0] = 2; r.T2d = q.T2d; }
+// extended -> affine Niels (one inversion)
+DEVI void ge_to_niels(gen &n, const ge &p) {
+    fe zi, x, y, t;
+    fe_invert(zi, p.Z);
+    fe_mul(x, p.X, zi); fe_mul(y, p.Y, zi);
+    fe_add(n.YpX, y, x); fe_sub(n.YmX, y, x);
+    fe_mul(t, x, y); fe_mul(n.T2d, t, FE_D2);
+    n.pad[0] = n.pad[1] = 0;
+}
 // extended + extended (cached form of q built on the fly, unreduced): 9M
 DEVI void ge_add(ge &r, const ge &p, const ge &q) {
     fe a, b, c, d, e, f, g, h, t;
@@ -573,30 +606,35 @@ DEVI void ristretto_elligator(ge &p, const fe &r0) {
 }
 
 // ---------------------------------------------------------------------------
-// memory helpers: points are 160 B (X,Y,Z,T as 10 limbs), moved as 10 x uint4
+// memory helpers: points move as 16-byte vectors (160 B extended/cached,
+// 128 B affine Niels)
 // ---------------------------------------------------------------------------
 template <class P>
 DEVI void pt_load(P &p, const P *src) {
-    static_assert(sizeof(P) == 160, "point layout");
+    static_assert(sizeof(P) % 16 == 0, "point layout");
+    constexpr int NQ = sizeof(P) / 16;
     const uint4 *s = reinterpret_cast<const uint4 *>(src);
-    uint4 q[10];
+    uint4 q[NQ];
 #pragma unroll
-    for (int i = 0; i < 10; i++) q[i] = s[i];
+    for (int i = 0; i < NQ; i++) q[i] = s[i];
     uint32_t *d = reinterpret_cast<uint32_t *>(&p);
 #pragma unroll
-    for (int i = 0; i < 10; i++) { d[4 * i] = q[i].x; d[4 * i + 1] = q[i].y; d[4 * i + 2] = q[i].z; d[4 * i + 3] = q[i].w; }
+    for (int i = 0; i < NQ; i++) { d[4 * i] = q[i].x; d[4 * i + 1] = q[i].y; d[4 * i + 2] = q[i].z; d[4 * i + 3] = q[i].w; }
 }
 template <class P>
 DEVI void pt_store(P *dst, const P &p) {
+    constexpr int NQ = sizeof(P) / 16;
     uint4 *d = reinterpret_cast<uint4 *>(dst);
     const uint32_t *s = reinterpret_cast<const uint32_t *>(&p);
 #pragma unroll
-    for (int i = 0; i < 10; i++) d[i] = make_uint4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
+    for (int i = 0; i < NQ; i++) d[i] = make_uint4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
 }
 DEVI void ge_load(ge &p, const ge *src) { pt_load(p, src); }
 DEVI void ge_store(ge *dst, const ge &p) { pt_store(dst, p); }
 DEVI void gec_load(gec &p, const gec *src) { pt_load(p, src); }
 DEVI void gec_store(gec *dst, const gec &p) { pt_store(dst, p); }
+DEVI void gen_load(gen &p, const gen *src) { pt_load(p, src); }
+DEVI void gen_store(gen *dst, const gen &p) { pt_store(dst, p); }
 DEVI void sc_load(sc &r, const sc *src) {
     const uint4 *s = reinterpret_cast<const uint4 *>(src);
     uint4 a = s[0], b = s[1];
@@ -607,4 +645,18 @@ DEVI void sc_store(sc *dst, const sc &a) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
     d[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
     d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+
+// Packed affine Niels (comb tables): three canonical field elements as
+// 8 little-endian words each, 96 B = 6 x uint4.
+DEVI void genp_store(uint4 *dst, const gen &q) {
+    uint32_t w[24];
+    fe_tow(w, q.YpX); fe_tow(w + 8, q.YmX); fe_tow(w + 16, q.T2d);
+#pragma unroll
+    for (int i = 0; i < 6; i++) dst[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+DEVI void genp_unpack(gen &q, const uint4 (&s)[6]) {
+    q.YpX = fe_from_words(s[0].x, s[0].y, s[0].z, s[0].w, s[1].x, s[1].y, s[1].z, s[1].w);
+    q.YmX = fe_from_words(s[2].x, s[2].y, s[2].z, s[2].w, s[3].x, s[3].y, s[3].z, s[3].w);
+    q.T2d = fe_from_words(s[4].x, s[4].y, s[4].z, s[4].w, s[5].x, s[5].y, s[5].z, s[5].w);
 }

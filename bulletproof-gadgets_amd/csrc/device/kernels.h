@@ -13,6 +13,8 @@ namespace dev {
 // points (X, Y, Z, T; each 10 limbs of 26/25 bits).
 struct ScD { uint32_t v[8]; };
 struct PtD { uint32_t v[40]; };
+// affine Niels (y+x, y-x, 2dxy), Z = 1: 3 x 10 limbs + 2 pad words = 128 B
+struct NielsD { uint32_t v[32]; };
 
 #define BPG_HIP(x)                                                                 \
     do {                                                                           \
@@ -28,20 +30,24 @@ struct HipError {
 };
 
 // -------------------------------------------------------------- points
-// Point arrays in HBM (generators, folded generators, decompressed inputs)
-// are cached points; MSM window rows returned to the host are extended.
+// Generators and decompressed inputs live in HBM as affine Niels points
+// (128 B, one line per random gather); folded generators are cached points
+// (160 B); MSM window rows returned to the host are extended.
 // out[i] = from_uniform_bytes(uniform[64*i .. 64*i+64))
-void launch_gens_map(const uint8_t *uniform, PtD *out, uint32_t count, hipStream_t st);
+void launch_gens_map(const uint8_t *uniform, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = v[i]*B + vb[i]*B_blinding using fixed-base tables (64 x 8 points each)
 void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tabB, const PtD *tabBb,
                      uint32_t *out_compressed, hipStream_t st);
-void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st);
-void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hipStream_t st);
+void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st);     // cached in
+void launch_compress(const NielsD *in, uint32_t *out, uint32_t count, hipStream_t st);  // Niels in
+void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count, hipStream_t st);
 
 // -------------------------------------------------------------- MSM
+#define MSM_CACHED 0   // bases are cached points (PtD)
+#define MSM_NIELS 1    // bases are affine Niels points (NielsD)
 struct MsmSeg {
     const ScD *scal;   // canonical scalars (< l)
-    const PtD *base;   // cached points (Y+X, Y-X, 2Z, 2dT)
+    const void *base;  // PtD (cached) or NielsD, per the job's format
     uint32_t count;
     uint32_t msm;      // which MSM of the job this segment contributes to
 };
@@ -68,8 +74,8 @@ class MsmEngine {
     // Enqueue a multi-MSM job on the stream; window-row sums land in
     // `rows_host` (pinned, nmsm * W points) when `done` fires.
     // Returns the plan (window width c and count W are needed by the host
-    // combine). Segments: at most 8.
-    MsmPlan enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host);
+    // combine). Segments: at most 12, all bases in format `fmt`.
+    MsmPlan enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt);
   private:
     void reserve(const MsmPlan &p);
     hipStream_t st_;
@@ -127,8 +133,34 @@ void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStr
 // (one per stream; the host side is rewritten only after the stream has
 // passed the previous use).
 struct ArgStage { void *dev = nullptr, *host = nullptr; hipEvent_t copied = nullptr; };
-void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
-                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage, hipStream_t st);
+// Gin/Hin: NielsD (in_fmt = MSM_NIELS, the generators) or PtD (MSM_CACHED)
+void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32_t h, uint32_t n, ScD rhoG_a,
+                            ScD rhoG_b, ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage,
+                            hipStream_t st);
+// Two-round table fold: G2_i = G_i + c1 G_{i+h1} + c2 G_{i+2h1} + c3 G_{i+3h1}
+// from comb tables of the level-0 generators j in [h1, 4h1) (likewise H).
+// Table entry (w, d) of table index jj = (d+1) 16^w P_{h1+jj}, packed affine
+// Niels, 96 B, at byte offset ((w*8+d)*ntab + jj)*96.
+#define COMB_MAXRANGE 8
+struct CombArgs {
+    const void *gens[2];       // G, H (NielsD), level 0
+    const void *tab[2];        // comb tables of G, H over [h1, 4 h1)
+    void *out[2];              // PtD (cached) outputs, h1 each
+    uint32_t h1, ntab;         // ntab = 3 h1
+    uint32_t nrange;           // lanes [rstart[r], rstart[r+1]) share digits
+    uint32_t rstart[COMB_MAXRANGE];
+    int8_t dig[2][COMB_MAXRANGE][3][64];   // signed radix-16 digits of c1, c2, c3
+};
+void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab, hipStream_t st);
+void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st);
+// Round 1 of the lazy schedule: level-1 generators expanded into level 0.
+struct LazyArgs {
+    uint32_t h0;              // round-0 half length (pairs j, j + h0)
+    ScD rGa, rGb, rHa, rHb;   // round-0 fold scalars (Montgomery), per class
+};
+// msm_scal[0..8h) (layout in kernels.hip), c_L -> [8h], c_R -> [8h+1]
+void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
+                          ScD *msm_scal, ScD *partial, hipStream_t st);
 // verifier helpers
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
                       ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st);

@@ -19,6 +19,7 @@ namespace dev {
 
 static_assert(sizeof(ScD) == sizeof(sc), "scalar layout");
 static_assert(sizeof(PtD) == sizeof(ge) && sizeof(PtD) == sizeof(gec), "point layout");
+static_assert(sizeof(NielsD) == sizeof(gen) && sizeof(gen) == 128, "niels layout");
 
 #define AS_SC(p) reinterpret_cast<sc *>(p)
 #define AS_CSC(p) reinterpret_cast<const sc *>(p)
@@ -26,13 +27,15 @@ static_assert(sizeof(PtD) == sizeof(ge) && sizeof(PtD) == sizeof(gec), "point la
 #define AS_CGE(p) reinterpret_cast<const ge *>(p)
 #define AS_GEC(p) reinterpret_cast<gec *>(p)
 #define AS_CGEC(p) reinterpret_cast<const gec *>(p)
+#define AS_GEN(p) reinterpret_cast<gen *>(p)
+#define AS_CGEN(p) reinterpret_cast<const gen *>(p)
 
 static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // ===========================================================================
 // point kernels
 // ===========================================================================
-__global__ __launch_bounds__(64) void k_gens_map(const uint32_t *__restrict__ uni, gec *__restrict__ out, uint32_t count) {
+__global__ __launch_bounds__(64) void k_gens_map(const uint32_t *__restrict__ uni, gen *__restrict__ out, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const uint32_t *w = uni + 16 * (size_t)i;
@@ -46,12 +49,12 @@ __global__ __launch_bounds__(64) void k_gens_map(const uint32_t *__restrict__ un
     ristretto_elligator(p1, r1);
     ristretto_elligator(p2, r2);
     ge_add(p, p1, p2);
-    gec c; ge_to_cached(c, p);
-    gec_store(out + i, c);
+    gen c; ge_to_niels(c, p);
+    gen_store(out + i, c);
 }
-void launch_gens_map(const uint8_t *uniform, PtD *out, uint32_t count, hipStream_t st) {
+void launch_gens_map(const uint8_t *uniform, NielsD *out, uint32_t count, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_gens_map, dim3(nblk(count, 64)), dim3(64), 0, st, (const uint32_t *)uniform, AS_GEC(out), count);
+    hipLaunchKernelGGL(k_gens_map, dim3(nblk(count, 64)), dim3(64), 0, st, (const uint32_t *)uniform, AS_GEN(out), count);
     BPG_HIP(hipGetLastError());
 }
 
@@ -107,19 +110,27 @@ void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tab
     BPG_HIP(hipGetLastError());
 }
 
-__global__ __launch_bounds__(64) void k_compress(const gec *__restrict__ in, uint32_t *__restrict__ out, uint32_t count) {
+DEVI void load_as_cached(gec &c, const gec *p) { gec_load(c, p); }
+DEVI void load_as_cached(gec &c, const gen *p) { gen q; gen_load(q, p); gen_to_cached(c, q); }
+template <class P>
+__global__ __launch_bounds__(64) void k_compress(const P *__restrict__ in, uint32_t *__restrict__ out, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    gec c; gec_load(c, in + i);
+    gec c; load_as_cached(c, in + i);
     ge p; ge_from_cached(p, c);
     ristretto_encode(out + 8 * (size_t)i, p);
 }
 void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_compress, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEC(in), out, count);
+    hipLaunchKernelGGL(k_compress<gec>, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEC(in), out, count);
     BPG_HIP(hipGetLastError());
 }
-__global__ __launch_bounds__(64) void k_decompress(const uint32_t *__restrict__ in, gec *__restrict__ out, int *ok, uint32_t count) {
+void launch_compress(const NielsD *in, uint32_t *out, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_compress<gen>, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(in), out, count);
+    BPG_HIP(hipGetLastError());
+}
+__global__ __launch_bounds__(64) void k_decompress(const uint32_t *__restrict__ in, gen *__restrict__ out, int *ok, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     uint32_t w[8];
@@ -128,12 +139,15 @@ __global__ __launch_bounds__(64) void k_decompress(const uint32_t *__restrict__ 
     ge p;
     bool good = ristretto_decode(p, w);
     if (!good) { ge_identity(p); atomicAnd(ok, 0); }
-    gec c; ge_to_cached(c, p);
-    gec_store(out + i, c);
+    // decoded points have Z = 1: affine Niels without an inversion
+    gen c;
+    fe_add(c.YpX, p.Y, p.X); fe_sub(c.YmX, p.Y, p.X); fe_mul(c.T2d, p.T, FE_D2);
+    c.pad[0] = c.pad[1] = 0;
+    gen_store(out + i, c);
 }
-void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hipStream_t st) {
+void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_decompress, dim3(nblk(count, 64)), dim3(64), 0, st, in, AS_GEC(out), ok, count);
+    hipLaunchKernelGGL(k_decompress, dim3(nblk(count, 64)), dim3(64), 0, st, in, AS_GEN(out), ok, count);
     BPG_HIP(hipGetLastError());
 }
 
@@ -155,17 +169,18 @@ void launch_decompress(const uint32_t *in, PtD *out, int *ok, uint32_t count, hi
 #define RBK_T 16
 #define RBK_BLOCK 256
 #define RBK_CHUNK (RBK_T * RBK_BLOCK)
+#define MSM_MAXSEG 12
 struct SegTab {
-    const sc *scal[8];
-    const gec *base[8];
-    uint32_t gofs[9];
-    uint32_t row0[8];
+    const sc *scal[MSM_MAXSEG];
+    const void *base[MSM_MAXSEG];
+    uint32_t gofs[MSM_MAXSEG + 1];
+    uint32_t row0[MSM_MAXSEG];
     int n;
 };
 DEVI int seg_of(const SegTab &T, uint32_t g) {
     int si = 0;
 #pragma unroll
-    for (int k = 1; k < 8; k++) if (k < T.n && g >= T.gofs[k]) si = k;
+    for (int k = 1; k < MSM_MAXSEG; k++) if (k < T.n && g >= T.gofs[k]) si = k;
     return si;
 }
 
@@ -250,32 +265,45 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_count(const uint32_t *__restr
     }
     cnt[j] = c;
 }
-__global__ void k_rbk_total(const uint32_t *cnt, const uint32_t *off, uint32_t nthreads, uint32_t *E_out) {
-    *E_out = off[nthreads - 1] + cnt[nthreads - 1];
-}
 
-DEVI void msm_gather(gec &p, const SegTab &T, uint32_t v) {
+// acc += +-base[v]: one gather of a cached (160 B) or affine Niels (128 B,
+// one line, 7M madd) base, by the job's base format
+template <int FMT>
+DEVI void msm_add_base(ge &acc, const SegTab &T, uint32_t v) {
     uint32_t g = v & 0x7fffffffu;
     int si = seg_of(T, g);
-    gec_load(p, T.base[si] + (g - T.gofs[si]));
-    gec_cneg(p, v >> 31);
+    if (FMT == MSM_NIELS) {
+        gen p;
+        gen_load(p, reinterpret_cast<const gen *>(T.base[si]) + (g - T.gofs[si]));
+        gen_cneg(p, v >> 31);
+        ge_madd(acc, acc, p);
+    } else {
+        gec p;
+        gec_load(p, reinterpret_cast<const gec *>(T.base[si]) + (g - T.gofs[si]));
+        gec_cneg(p, v >> 31);
+        ge_add_c(acc, acc, p);
+    }
 }
 // Sum runs. FIRST: entries are (key, signed base index); else entries are
 // pieces (key, extended partial at the same index) from the previous pass.
-template <bool FIRST>
+template <bool FIRST, int FMT>
 __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_sum(const uint32_t *__restrict__ keys,
                                                        const uint32_t *__restrict__ vals,
                                                        const ge *__restrict__ pin, SegTab T, uint64_t E_host,
                                                        const uint32_t *E_dev, uint32_t invalid,
-                                                       const uint32_t *__restrict__ off, uint32_t *__restrict__ kout,
+                                                       const uint32_t *__restrict__ off,
+                                                       const uint32_t *__restrict__ cnt, uint32_t nthr,
+                                                       uint32_t *__restrict__ E_out, uint32_t *__restrict__ kout,
                                                        ge *__restrict__ pout, ge *__restrict__ buckets,
                                                        uint8_t *__restrict__ bflag) {
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
     __shared__ uint32_t sv[FIRST ? RBK_CHUNK + RBK_BLOCK : 1];
+    const uint32_t t = threadIdx.x;
+    // pieces this pass leaves (the next pass's entry count)
+    if (blockIdx.x * RBK_BLOCK + t == nthr - 1) *E_out = off[nthr - 1] + cnt[nthr - 1];
     const uint64_t E = rbk_E(E_host, E_dev);
     const uint64_t base = (uint64_t)blockIdx.x * RBK_CHUNK;
     if (base >= E) return;
-    const uint32_t t = threadIdx.x;
     rbk_stage(sk, keys, base, E, invalid);
     if (FIRST) {
         for (uint32_t k = t; k < RBK_CHUNK; k += RBK_BLOCK) {
@@ -305,8 +333,7 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_sum(const uint32_t *__restric
             ge_identity(acc);
         }
         if (FIRST) {
-            gec p; msm_gather(p, T, sv[rbk_lds(t * RBK_T + i)]);
-            ge_add_c(acc, acc, p);
+            msm_add_base<FMT>(acc, T, sv[rbk_lds(t * RBK_T + i)]);
         } else {
             ge p; ge_load(p, pin + gs + i);
             ge_add(acc, acc, p);
@@ -460,8 +487,9 @@ void MsmEngine::reserve(const MsmPlan &p) {
     rows_dev_.grow((size_t)p.rows * sizeof(ge));
 }
 
-MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host) {
-    if (nseg < 1 || nseg > 8) throw HipError(hipErrorInvalidValue, "nseg", __FILE__, __LINE__);
+MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt) {
+    if (nseg < 1 || nseg > MSM_MAXSEG) throw HipError(hipErrorInvalidValue, "nseg", __FILE__, __LINE__);
+    if (fmt != MSM_NIELS && fmt != MSM_CACHED) throw HipError(hipErrorInvalidValue, "fmt", __FILE__, __LINE__);
     MsmPlan p{};
     SegTab T{};
     uint64_t total = 0;
@@ -476,7 +504,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     p.half = 1 << (p.c - 1);
     for (int i = 0; i < nseg; i++) {
         T.scal[i] = AS_CSC(segs[i].scal);
-        T.base[i] = AS_CGEC(segs[i].base);
+        T.base[i] = segs[i].base;
         T.row0[i] = segs[i].msm * p.W;
     }
     p.E0 = (uint64_t)p.W * total;
@@ -487,9 +515,12 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     while ((1ULL << p.key_bits) <= D) p.key_bits++;
     // pieces after a pass: at most 2 per thread chunk
     p.capE = std::min<uint64_t>(p.E0, 2 * ((p.E0 + RBK_T - 1) / RBK_T) + 2);
-    // passes: enough that T^passes exceeds the largest possible run (total)
+    // passes: each leaves at most 2 pieces per 16-entry chunk, so runs of
+    // random-looking digits (<~100 entries) are whole after two; a giant run
+    // (structured scalars, e.g. all 0/1) still completes in k_rbk_final,
+    // whose run head sums the remaining pieces serially.
     p.passes = 1;
-    { uint64_t r = RBK_T / 2; while (r < total + 1) { r *= RBK_T / 2; p.passes++; } }
+    { uint64_t r = RBK_T / 2; while (r < total + 1 && p.passes < 3) { r *= RBK_T / 2; p.passes++; } }
     p.seglen = p.half < 8 ? p.half : 8;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
@@ -534,13 +565,15 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         hipLaunchKernelGGL(k_rbk_count, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, Ebound, Ein, invalid, cnt);
         size_t tb = p.scan_tmp;
         BPG_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp_.p, tb, cnt, off, (int)nthr, st_));
-        hipLaunchKernelGGL(k_rbk_total, dim3(1), dim3(1), 0, st_, cnt, off, nthr, Ed + pass);
-        if (pass == 0)
-            hipLaunchKernelGGL(k_rbk_sum<true>, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, (const uint32_t *)vals2,
-                               pin, T, Ebound, Ein, invalid, off, kout, pout, buckets, bflag);
+        if (pass == 0 && fmt == MSM_NIELS)
+            hipLaunchKernelGGL((k_rbk_sum<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
+                               (const uint32_t *)vals2, pin, T, Ebound, Ein, invalid, off, cnt, nthr, Ed + pass, kout, pout, buckets, bflag);
+        else if (pass == 0)
+            hipLaunchKernelGGL((k_rbk_sum<true, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
+                               (const uint32_t *)vals2, pin, T, Ebound, Ein, invalid, off, cnt, nthr, Ed + pass, kout, pout, buckets, bflag);
         else
-            hipLaunchKernelGGL(k_rbk_sum<false>, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, (const uint32_t *)vals2,
-                               pin, T, Ebound, Ein, invalid, off, kout, pout, buckets, bflag);
+            hipLaunchKernelGGL((k_rbk_sum<false, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
+                               (const uint32_t *)vals2, pin, T, Ebound, Ein, invalid, off, cnt, nthr, Ed + pass, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
         Ein = Ed + pass;
         Ebound = std::min<uint64_t>(Ebound, p.capE);
@@ -898,7 +931,7 @@ struct FoldSched {
     uint8_t gap[64];          // doublings before dig[k] (gap[0] unused)
 };
 struct FoldArgs {
-    const gec *in[2];
+    const void *in[2];
     gec *out[2];
     uint32_t h, nseg;
     uint32_t start[6], end[6], blk0[7];
@@ -948,8 +981,11 @@ DEVI void fold_pick(gec &t, const gec &t1, const gec &t3, const gec &t5, const g
     if (m == 1) t = t1; else if (m == 3) t = t3; else if (m == 5) t = t5; else t = t7;
 }
 #ifndef BPG_FOLD_WAVES
-#define BPG_FOLD_WAVES 1
+#define BPG_FOLD_WAVES 2
 #endif
+// P: input point type (gen = affine Niels generators in round 0 of the
+// table-less path, gec = folded generators); the output is always cached.
+template <class P>
 __global__ __launch_bounds__(64, BPG_FOLD_WAVES) void k_ipp_fold_points(const FoldArgs *__restrict__ Ap) {
     const FoldArgs &A = *Ap;
     uint32_t b = blockIdx.x, sg = 0;
@@ -959,16 +995,16 @@ __global__ __launch_bounds__(64, BPG_FOLD_WAVES) void k_ipp_fold_points(const Fo
     if (i >= A.end[sg]) return;
     const uint32_t v = A.vec[sg];
     const FoldSched &S = A.sc[A.sched[sg]];
-    const gec *P = A.in[v];
+    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
     gec PL;
     if (S.ndig == 0) {
-        gec_load(PL, P + i);
+        load_as_cached(PL, Pin + i);
         gec_store(A.out[v] + i, PL);
         return;
     }
     gec t1, t3, t5, t7;
     {
-        gec_load(t1, P + A.h + i);
+        load_as_cached(t1, Pin + A.h + i);
         ge pr, p2, q;
         fe_sub(pr.X, t1.YpX, t1.YmX);            // projective (2X : 2Y : 2Z), enough to double
         fe_add(pr.Y, t1.YpX, t1.YmX);
@@ -997,13 +1033,14 @@ __global__ __launch_bounds__(64, BPG_FOLD_WAVES) void k_ipp_fold_points(const Fo
         for (uint32_t j = 1; j < S.tail; j++) ge_dbl_t<false>(acc, acc);
         ge_dbl_t<true>(acc, acc);
     }
-    gec_load(PL, P + i);
+    load_as_cached(PL, Pin + i);
     ge r; ge_add_c(r, acc, PL);
     gec out; ge_to_cached(out, r);
     gec_store(A.out[v] + i, out);
 }
-void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t n, ScD rhoG_a, ScD rhoG_b,
-                            ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage, hipStream_t st) {
+void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32_t h, uint32_t n, ScD rhoG_a,
+                            ScD rhoG_b, ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage,
+                            hipStream_t st) {
     if (!stage.dev) {
         BPG_HIP(hipMalloc(&stage.dev, sizeof(FoldArgs)));
         BPG_HIP(hipHostMalloc(&stage.host, sizeof(FoldArgs), hipHostMallocDefault));
@@ -1013,7 +1050,7 @@ void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t
     }
     FoldArgs &A = *reinterpret_cast<FoldArgs *>(stage.host);
     A = FoldArgs{};
-    A.in[0] = AS_CGEC(Gin); A.in[1] = AS_CGEC(Hin);
+    A.in[0] = Gin; A.in[1] = Hin;
     A.out[0] = AS_GEC(Gout); A.out[1] = AS_GEC(Hout);
     A.h = h;
     wnaf4_schedule(rhoG_a, A.sc[0]); wnaf4_schedule(rhoG_b, A.sc[1]);
@@ -1035,9 +1072,161 @@ void launch_ipp_fold_points(const PtD *Gin, const PtD *Hin, uint32_t h, uint32_t
     if (!blocks) return;
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldArgs), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
-    hipLaunchKernelGGL(k_ipp_fold_points, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
+    if (in_fmt == MSM_NIELS)
+        hipLaunchKernelGGL(k_ipp_fold_points<gen>, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
+    else
+        hipLaunchKernelGGL(k_ipp_fold_points<gec>, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }
+// ---------------------------------------------------------------------------
+// Comb tables and the two-round table fold (DESIGN.md "IPP rounds 0-1").
+// For generator j = j0 + jj (jj < ntab): entry (w, d) = (d+1) 16^w P_j for
+// w < 64, d < 8, packed affine Niels (96 B) at 16-byte unit
+// ((w*8 + d) * ntab + jj) * 6 — entry-major, so lanes that read the same
+// entry of consecutive generators read one contiguous span.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_comb_build(const gen *__restrict__ gens, uint32_t j0, uint32_t ntab,
+                                                   uint4 *__restrict__ tab) {
+    const uint32_t jj = blockIdx.x * blockDim.x + threadIdx.x;
+    if (jj >= ntab) return;
+    gen g;
+    gen_load(g, gens + j0 + jj);
+    gec c;
+    gen_to_cached(c, g);
+    ge pw;
+    ge_from_cached(pw, c);
+    for (int w = 0; w < 64; w++) {
+        gec pc;
+        ge_to_cached(pc, pw);
+        ge q = pw;
+        for (int d = 0; d < 8; d++) {
+            if (d) ge_add_c(q, q, pc);
+            gen e;
+            ge_to_niels(e, q);
+            genp_store(tab + ((size_t)(w * 8 + d) * ntab + jj) * 6, e);
+        }
+        ge_dbl(pw, q);   // 16^(w+1) P
+    }
+}
+void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab, hipStream_t st) {
+    if (!ntab) return;
+    hipLaunchKernelGGL(k_comb_build, dim3(nblk(ntab, 64)), dim3(64), 0, st, AS_CGEN(gens), j0, ntab,
+                       reinterpret_cast<uint4 *>(tab));
+    BPG_HIP(hipGetLastError());
+}
+
+// Output lane i < h1 of vector v (0 = G, 1 = H):
+//   out_i = P_i + sum_{t<3} c_t * P_{i + (t+1) h1}
+// with per-lane-range coefficient digits (signed radix 16, LSB first); no
+// doublings: every nonzero digit is one table read and one 7M madd.
+__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restrict__ Ap) {
+    const CombArgs &A = *Ap;
+    const uint32_t nb = (A.h1 + 63) / 64;
+    const uint32_t v = blockIdx.x >= nb ? 1 : 0;
+    const uint32_t i = (blockIdx.x - v * nb) * 64 + threadIdx.x;
+    if (i >= A.h1) return;
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 1; k < COMB_MAXRANGE; k++) if (k < (int)A.nrange && i >= A.rstart[k]) r = k;
+    const uint4 *tab = reinterpret_cast<const uint4 *>(A.tab[v]);
+    ge acc;
+    ge_identity(acc);
+    {
+        gen p;
+        gen_load(p, reinterpret_cast<const gen *>(A.gens[v]) + i);
+        ge_madd(acc, acc, p);
+    }
+    for (int t = 0; t < 3; t++) {
+        const uint32_t jj = i + (uint32_t)t * A.h1;
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(A.dig[v][r][t]);
+        for (int w4 = 0; w4 < 16; w4++) {
+            const uint32_t packed = dw[w4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int d = (int)(int8_t)(packed >> (8 * k));
+                if (d == 0) continue;
+                const int w = 4 * w4 + k;
+                const int m = d < 0 ? -d : d;
+                const uint4 *e = tab + ((size_t)(w * 8 + m - 1) * A.ntab + jj) * 6;
+                uint4 q[6];
+#pragma unroll
+                for (int u = 0; u < 6; u++) q[u] = e[u];
+                gen p;
+                genp_unpack(p, q);
+                gen_cneg(p, d < 0);
+                ge_madd(acc, acc, p);
+            }
+        }
+    }
+    gec out;
+    ge_to_cached(out, acc);
+    gec_store(reinterpret_cast<gec *>(A.out[v]) + i, out);
+}
+void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st) {
+    if (!args.h1) return;
+    if (!stage.dev) {
+        BPG_HIP(hipMalloc(&stage.dev, sizeof(CombArgs)));
+        BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombArgs), hipHostMallocDefault));
+        BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
+    } else {
+        BPG_HIP(hipEventSynchronize(stage.copied));
+    }
+    memcpy(stage.host, &args, sizeof(CombArgs));
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombArgs), hipMemcpyHostToDevice, st));
+    BPG_HIP(hipEventRecord(stage.copied, st));
+    const uint32_t nb = (args.h1 + 63) / 64;
+    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, reinterpret_cast<const CombArgs *>(stage.dev));
+    BPG_HIP(hipGetLastError());
+}
+
+// IPP round 1 with the level-1 generators left unmaterialised: each base of
+// the round, G1_j = G_j + rho0(j) G_{j+h0} (likewise H), is expanded into its
+// two level-0 generators, so the round's MSM scalars double (8h of them).
+// Layout: [L: G_A | G_B | H_A | H_B | R: G_A | G_B | H_A | H_B], c_L at 8h,
+// c_R at 8h+1. rho0 classes as in the fold (pair straddles n -> *_b).
+__global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                       const sc *__restrict__ yipm, IppRoundArgs A, LazyArgs Z,
+                                                       sc *__restrict__ out, sc *__restrict__ partial) {
+    sc acc[2];
+    sc_zero(acc[0]); sc_zero(acc[1]);
+    const uint32_t h = A.h, h0 = Z.h0, n = A.n;
+    const sc lamG1 = *reinterpret_cast<const sc *>(&A.lamG1), lamGu = *reinterpret_cast<const sc *>(&A.lamGu);
+    const sc muH1 = *reinterpret_cast<const sc *>(&A.muH1), muHu = *reinterpret_cast<const sc *>(&A.muHu);
+    const sc rGa = *reinterpret_cast<const sc *>(&Z.rGa), rGb = *reinterpret_cast<const sc *>(&Z.rGb);
+    const sc rHa = *reinterpret_cast<const sc *>(&Z.rHa), rHb = *reinterpret_cast<const sc *>(&Z.rHb);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < h; i += gridDim.x * blockDim.x) {
+        sc aL, aR, bL, bR, t, u, y;
+        sc_load(aL, a + i); sc_load(aR, a + h + i); sc_load(bL, b + i); sc_load(bR, b + h + i);
+        mm(t, aL, bR); sc_add(acc[0], acc[0], t);
+        mm(t, aR, bL); sc_add(acc[1], acc[1], t);
+        const uint32_t lo = i, hi = h + i;
+        const bool lo_real = lo < n, hi_real = hi < n;
+        const bool lo_b = lo < n && lo + h0 >= n, hi_b = hi < n && hi + h0 >= n;
+        // L, G part: base G1_{h+i}
+        mm(t, aL, hi_real ? lamG1 : lamGu); sc_store(out + i, t);
+        mm(u, t, hi_b ? rGb : rGa); sc_store(out + h + i, u);
+        // L, H part: base H1_i
+        sc_load(y, yipm + lo); mm(t, bR, y); mm(t, t, lo_real ? muH1 : muHu); sc_store(out + 2 * h + i, t);
+        mm(u, t, lo_b ? rHb : rHa); sc_store(out + 3 * h + i, u);
+        // R, G part: base G1_i
+        mm(t, aR, lo_real ? lamG1 : lamGu); sc_store(out + 4 * h + i, t);
+        mm(u, t, lo_b ? rGb : rGa); sc_store(out + 5 * h + i, u);
+        // R, H part: base H1_{h+i}
+        sc_load(y, yipm + hi); mm(t, bL, y); mm(t, t, hi_real ? muH1 : muHu); sc_store(out + 6 * h + i, t);
+        mm(u, t, hi_b ? rHb : rHa); sc_store(out + 7 * h + i, u);
+    }
+    block_reduce_store<2>(acc, partial);
+}
+void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
+                          ScD *msm_scal, ScD *partial, hipStream_t st) {
+    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
+    hipLaunchKernelGGL(k_ipp_prep_lazy, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, lz,
+                       AS_SC(msm_scal), AS_SC(partial));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
+                       AS_SC(msm_scal + 8 * (size_t)args.h), 1u, 0);
+    BPG_HIP(hipGetLastError());
+}
+
 __global__ void k_fill_scalars(sc *dst, sc val, uint32_t count) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) sc_store(dst + i, val);

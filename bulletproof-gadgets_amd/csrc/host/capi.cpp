@@ -67,6 +67,11 @@ void bpg_set_seed(uint64_t seed) {
     e.cs.seed(seed);
 }
 void bpg_clear_seed(void) { thread_entropy().seeded = false; }
+int bpg_set_fold_tables(int mode) {
+    if (mode < -1 || mode > 1) return -1;
+    set_fold_tables(mode);
+    return 0;
+}
 int bpg_set_device(int device) {
     if (device < 0) return -1;
     g_device = device;

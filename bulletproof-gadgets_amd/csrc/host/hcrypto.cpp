@@ -347,6 +347,31 @@ void pt_to_dev_cached(uint32_t w[40], const Point &p) {
     fe_to_w(w, ypx); fe_to_w(w + 10, ymx); fe_to_w(w + 20, z2); fe_to_w(w + 30, t2d);
 }
 
+void pt_to_dev_niels(uint32_t w[32], const Point &p) {
+    Fe t19, t3, zi, x, y, t, ypx, ymx, t2d;
+    fpow22501(t19, t3, p.Z); fsqn(t19, t19, 5); fmul(zi, t19, t3);   // Z^(p-2)
+    fmul(x, p.X, zi); fmul(y, p.Y, zi);
+    fadd(ypx, y, x); fsub(ymx, y, x); fmul(t, x, y); fmul(t2d, t, FD2);
+    fe_to_w(w, ypx); fe_to_w(w + 10, ymx); fe_to_w(w + 20, t2d);
+    w[30] = w[31] = 0;
+}
+void pt_from_dev_niels(Point &p, const uint32_t w[32]) {
+    Fe ypx, ymx, two, t;
+    fe_from_w(ypx, w); fe_from_w(ymx, w + 10);
+    // (2x : 2y : 2 : ...) -> extended (X Z : Y Z : Z^2 : X Y) with Z = 2
+    Fe x2, y2;
+    fsub(x2, ypx, ymx); fadd(y2, ypx, ymx);
+    two = FE1; fadd(two, two, two);
+    fmul(p.X, x2, two); fmul(p.Y, y2, two); fmul(p.Z, two, two); fmul(p.T, x2, y2);
+    (void)t;
+}
+void radix16_digits(const Scalar &s0, int8_t e[64]) {
+    Scalar s = s0.reduced();
+    uint8_t b[32]; s.to_bytes(b);
+    for (int i = 0; i < 32; i++) { e[2 * i] = b[i] & 15; e[2 * i + 1] = (b[i] >> 4) & 15; }
+    for (int i = 0; i < 63; i++) { int8_t c = (e[i] + 8) >> 4; e[i] -= c << 4; e[i + 1] += c; }
+}
+
 static const uint8_t BASEPOINT_COMPRESSED[32] = {
     0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9, 0x61, 0xc5, 0x00, 0x51, 0x5f,
     0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82, 0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};

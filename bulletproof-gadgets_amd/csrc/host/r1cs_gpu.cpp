@@ -5,6 +5,8 @@
 // and src/r1cs/proof.rs `to_bytes` / `from_bytes`.
 #include "r1cs_gpu.h"
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -65,9 +67,9 @@ void DeviceContext::ensure_gens(uint32_t N) {
     if (N <= gens_cap) return;
     uint32_t cap = std::max<uint32_t>(N, 64);
     BPG_HIP(hipSetDevice(device));
-    PtD *nG = nullptr, *nH = nullptr;
-    BPG_HIP(hipMalloc(&nG, (size_t)cap * sizeof(PtD)));
-    BPG_HIP(hipMalloc(&nH, (size_t)cap * sizeof(PtD)));
+    NielsD *nG = nullptr, *nH = nullptr;
+    BPG_HIP(hipMalloc(&nG, (size_t)cap * sizeof(NielsD)));
+    BPG_HIP(hipMalloc(&nH, (size_t)cap * sizeof(NielsD)));
     std::vector<uint8_t> uni((size_t)cap * 64);
     uint8_t *duni = nullptr;
     BPG_HIP(hipMalloc(&duni, uni.size()));
@@ -87,6 +89,47 @@ void DeviceContext::ensure_gens(uint32_t N) {
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
     G = nG; H = nH; gens_cap = cap;
+}
+
+static std::atomic<int> g_fold_tables(-1);
+void set_fold_tables(int mode) { g_fold_tables = mode; }
+static bool fold_tables_enabled() {
+    int m = g_fold_tables;
+    if (m >= 0) return m != 0;
+    const char *e = getenv("BPG_FOLD_TABLES");
+    return !(e && e[0] == '0');
+}
+CombTables::~CombTables() {
+    if (tabG || tabH) (void)hipSetDevice(device);
+    if (tabG) (void)hipFree(tabG);
+    if (tabH) (void)hipFree(tabH);
+}
+std::shared_ptr<CombTables> DeviceContext::ensure_comb(uint32_t N) {
+    if (N < 8 || !fold_tables_enabled()) return nullptr;
+    ensure_gens(N);
+    std::lock_guard<std::mutex> lk(mu);
+    if (comb && comb->N == N) return comb;
+    const uint32_t h1 = N / 4, ntab = 3 * h1;
+    const size_t bytes = (size_t)ntab * 512 * 96;   // per vector
+    BPG_HIP(hipSetDevice(device));
+    comb.reset();   // tables for another N are released once their users finish
+    size_t free_b = 0, total_b = 0;
+    BPG_HIP(hipMemGetInfo(&free_b, &total_b));
+    const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 8);   // per-thread workspaces
+    if (2 * bytes + reserve > free_b) return nullptr;
+    std::shared_ptr<CombTables> t(new CombTables());
+    t->device = device;
+    t->N = N;
+    t->bytes = 2 * bytes;
+    if (hipMalloc(&t->tabG, bytes) != hipSuccess || hipMalloc(&t->tabH, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    launch_comb_build(G, h1, ntab, t->tabG, 0);
+    launch_comb_build(H, h1, ntab, t->tabH, 0);
+    BPG_HIP(hipDeviceSynchronize());
+    comb = t;
+    return comb;
 }
 
 // ---------------------------------------------------------- instrumentation
@@ -116,6 +159,7 @@ struct Workspace {
     size_t s_host_cap = 0;
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
     dev::ArgStage fold_stage;        // IPP fold kernel arguments
+    dev::ArgStage comb_stage;        // table-fold kernel arguments
     hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
     void sync() {
         BPG_HIP(hipEventRecord(done_ev, st));
@@ -126,6 +170,9 @@ struct Workspace {
         if (fold_stage.dev) (void)hipFree(fold_stage.dev);
         if (fold_stage.host) (void)hipHostFree(fold_stage.host);
         if (fold_stage.copied) (void)hipEventDestroy(fold_stage.copied);
+        if (comb_stage.dev) (void)hipFree(comb_stage.dev);
+        if (comb_stage.host) (void)hipHostFree(comb_stage.host);
+        if (comb_stage.copied) (void)hipEventDestroy(comb_stage.copied);
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
@@ -294,6 +341,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
         up(P->vb_dev, vbd.data(), (size_t)m * sizeof(ScD));
         P->V.resize((size_t)m * 32);
         if (m) gpu_pedersen(device, P->v, P->vb, P->V.data());
+        DeviceContext::get(device).ensure_comb(P->N);   // circuit-independent, outside any timed region
     }
     return P;
 }
@@ -330,7 +378,7 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
     DeviceContext::get(device);
     Workspace &ws = thread_workspace(device);
     ws.small.grow((size_t)n * sizeof(ScD) + 64);
-    ws.pts.grow((size_t)n * sizeof(PtD) + 64);
+    ws.pts.grow((size_t)n * sizeof(NielsD) + 64);
     ws.okflag.grow(64);
     std::vector<ScD> s(n ? n : 1);
     for (uint32_t i = 0; i < n; i++) s[i] = to_dev(Scalar::reduce(scalars + 32 * (size_t)i));
@@ -340,11 +388,11 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
     BPG_HIP(hipMemcpyAsync(ws.gh.p, points, (size_t)n * 32, hipMemcpyHostToDevice, ws.st));
     int one = 1;
     BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, ws.st));
-    launch_decompress(as<uint32_t>(ws.gh), as<PtD>(ws.pts), as<int>(ws.okflag), n, ws.st);
+    launch_decompress(as<uint32_t>(ws.gh), as<NielsD>(ws.pts), as<int>(ws.okflag), n, ws.st);
     int ok = 0;
     BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, ws.st));
-    MsmSeg seg{as<ScD>(ws.small), as<PtD>(ws.pts), n, 0};
-    MsmPlan p = ws.msm->enqueue(&seg, 1, 1, ws.rows_host);
+    MsmSeg seg{as<ScD>(ws.small), ws.pts.p, n, 0};
+    MsmPlan p = ws.msm->enqueue(&seg, 1, 1, ws.rows_host, MSM_NIELS);
     ws.sync();
     if (!ok) return -1;
     Point r;
@@ -512,7 +560,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                           {as<ScD>(const_cast<DBuf &>(cs.aR)), ctx.H, n, 0},
                           {as<ScD>(const_cast<DBuf &>(cs.aO)), ctx.G, n, 1}};
         int ph = ws.prof_begin("msm_commit", 3.0 * n * (64 + 32));
-        pA = ws.msm->enqueue(segA, 3, 2, rowsA);
+        pA = ws.msm->enqueue(segA, 3, 2, rowsA, MSM_NIELS);
         ws.prof_end(ph);
     }
     // s_L | s_R: raw 64-byte draws -> device, reduced mod l there
@@ -529,7 +577,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         launch_wide_reduce(wd + 64 * (size_t)n, n, as<ScD>(ws.sR), st);
         MsmSeg segS[2] = {{as<ScD>(ws.sL), ctx.G, n, 0}, {as<ScD>(ws.sR), ctx.H, n, 0}};
         int ph = ws.prof_begin("msm_commit", 2.0 * n * (64 + 32));
-        pS = ws.msm->enqueue(segS, 2, 1, rowsS);
+        pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
         ws.prof_end(ph);
     }
     ws.sync();
@@ -631,25 +679,40 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     T.append_scalar("e_blinding", e_bl);
     Scalar wch = T.challenge_scalar("w");
     Point Qp; mul_B(Qp, wch);
-    ws.Q.grow(sizeof(PtD));
-    PtD Qd; pt_to_dev_cached(Qd.v, Qp);
-    BPG_HIP(hipMemcpyAsync(ws.Q.p, &Qd, sizeof(PtD), hipMemcpyHostToDevice, st));
+    // Q in both base formats: cached for jobs over folded generators, affine
+    // Niels for jobs over the level-0 generators
+    ws.Q.grow(sizeof(PtD) + sizeof(NielsD));
+    {
+        uint8_t qb[sizeof(PtD) + sizeof(NielsD)];
+        pt_to_dev_cached(reinterpret_cast<uint32_t *>(qb), Qp);
+        pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD)), Qp);
+        memcpy(ws.small_host + 3000, qb, sizeof(qb));
+        BPG_HIP(hipMemcpyAsync(ws.Q.p, ws.small_host + 3000, sizeof(qb), hipMemcpyHostToDevice, st));
+    }
+    const PtD *Qc = as<PtD>(ws.Q);
+    const NielsD *Qn = reinterpret_cast<const NielsD *>(as<uint8_t>(ws.Q) + sizeof(PtD));
     ws.a.grow((size_t)N * sizeof(ScD) + 64);
     ws.b.grow((size_t)N * sizeof(ScD) + 64);
     launch_lr_eval(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0), as<ScD>(ws.r1),
                    as<ScD>(ws.r3), as<ScD>(ws.ypm), n, N, mont(x), mont(x * x), as<ScD>(ws.a), as<ScD>(ws.b), st);
     double t2 = now_ms();
 
-    // InnerProductProof::create with weighted single-scalar point folding
+    // InnerProductProof::create with weighted single-scalar point folding.
+    // With comb tables (N >= 8) rounds 0 and 1 leave the level-1 generators
+    // unmaterialised: round 1's MSM expands them into level-0 generators and
+    // level 2 is built in one table pass.
     T.append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
     T.append_u64("n", N);
+    std::shared_ptr<CombTables> comb = ctx.ensure_comb(N);
     std::vector<uint8_t> LRc(64 * (size_t)lgN);
     Scalar lam = Scalar::one(), mu = Scalar::one();
-    const PtD *Gh = ctx.G, *Hh = ctx.H;
+    const void *Gh = ctx.G, *Hh = ctx.H;
+    int gfmt = MSM_NIELS;
     ws.mscal.grow((size_t)(2 * N + 2) * sizeof(ScD) + 64);
     if (N >= 2) {
         for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(N / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(N / 2) * sizeof(PtD)); }
     }
+    Scalar rho0[4];   // round-0 fold scalars (G a/b, H a/b) for the table pass
     uint32_t len = N;
     for (uint32_t k = 0; len != 1; k++) {
         const uint32_t h = len / 2;
@@ -658,13 +721,36 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         A.lamG1 = mont(lam); A.lamGu = mont(lam * u);
         A.muH1 = mont(mu); A.muHu = mont(mu * u);
         ScD *ms = as<ScD>(ws.mscal);
-        launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-        const PtD *Qdev = as<PtD>(ws.Q);
-        MsmSeg seg[6] = {{ms, Gh + h, h, 0}, {ms + h, Hh, h, 0}, {ms + 4 * (size_t)h, Qdev, 1, 0},
-                         {ms + 2 * (size_t)h, Gh, h, 1}, {ms + 3 * (size_t)h, Hh + h, h, 1},
-                         {ms + 4 * (size_t)h + 1, Qdev, 1, 1}};
-        int ph = ws.prof_begin("msm_ipp", (4.0 * h + 2) * (64 + 32));
-        MsmPlan pl = ws.msm->enqueue(seg, 6, 2, rowsLR);
+        const void *Qb = gfmt == MSM_NIELS ? (const void *)Qn : (const void *)Qc;
+        MsmSeg seg[10];
+        int nseg;
+        const bool lazy = comb && k == 1;
+        if (lazy) {
+            const uint32_t h0 = 2 * h;
+            LazyArgs Z;
+            Z.h0 = h0;
+            Z.rGa = mont(rho0[0]); Z.rGb = mont(rho0[1]); Z.rHa = mont(rho0[2]); Z.rHb = mont(rho0[3]);
+            launch_ipp_prep_lazy(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
+            const NielsD *G0 = ctx.G, *H0 = ctx.H;
+            const size_t hh = h;
+            MsmSeg sl[10] = {{ms, G0 + h, h, 0}, {ms + hh, G0 + h + h0, h, 0}, {ms + 2 * hh, H0, h, 0},
+                             {ms + 3 * hh, H0 + h0, h, 0}, {ms + 8 * hh, Qb, 1, 0},
+                             {ms + 4 * hh, G0, h, 1}, {ms + 5 * hh, G0 + h0, h, 1}, {ms + 6 * hh, H0 + h, h, 1},
+                             {ms + 7 * hh, H0 + h + h0, h, 1}, {ms + 8 * hh + 1, Qb, 1, 1}};
+            std::copy(sl, sl + 10, seg);
+            nseg = 10;
+        } else {
+            launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
+            const size_t ps = gfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
+            auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
+            const size_t hh = h;
+            MsmSeg sl[6] = {{ms, at(Gh, h), h, 0}, {ms + hh, Hh, h, 0}, {ms + 4 * hh, Qb, 1, 0},
+                            {ms + 2 * hh, Gh, h, 1}, {ms + 3 * hh, at(Hh, h), h, 1}, {ms + 4 * hh + 1, Qb, 1, 1}};
+            std::copy(sl, sl + 6, seg);
+            nseg = 6;
+        }
+        int ph = ws.prof_begin("msm_ipp", ((lazy ? 8.0 : 4.0) * h + 2) * (64 + 32));
+        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, gfmt);
         ws.prof_end(ph);
         ws.sync();
         Point Lp, Rp;
@@ -678,15 +764,53 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         Scalar uk = T.challenge_scalar("u");
         Scalar uinv = sc_invert(uk);
         launch_ipp_fold_scalars(as<ScD>(ws.a), as<ScD>(ws.b), h, mont(uk), mont(uinv), st);
-        if (h > 1) {
-            Scalar u2 = uk * uk, ui2 = uinv * uinv;
-            Scalar yh = sc_pow_u64(y_inv, h);
-            Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
+        Scalar u2 = uk * uk, ui2 = uinv * uinv;
+        Scalar yh = sc_pow_u64(y_inv, h);
+        Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
+        if (comb && k == 0) {
+            rho0[0] = rGa; rho0[1] = rGb; rho0[2] = rHa; rho0[3] = rHb;   // level 1 stays implicit
+        } else if (lazy && h > 1) {
+            // level 2 from level 0: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
+            const uint32_t h1 = h, h0 = 2 * h;
+            CombArgs C{};
+            C.gens[0] = ctx.G; C.gens[1] = ctx.H;
+            C.tab[0] = comb->tabG; C.tab[1] = comb->tabH;
+            C.out[0] = ws.Gp[1].p; C.out[1] = ws.Hp[1].p;
+            C.h1 = h1; C.ntab = 3 * h1;
+            std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)n - h1, (int64_t)n, (int64_t)n - h0,
+                                        (int64_t)n - h0 - h1};
+            std::vector<uint32_t> starts;
+            for (int64_t c : cut) if (c >= 0 && c < (int64_t)h1) starts.push_back((uint32_t)c);
+            std::sort(starts.begin(), starts.end());
+            starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+            C.nrange = (uint32_t)starts.size();
+            const Scalar r1[4] = {rGa, rGb, rHa, rHb};
+            for (uint32_t r = 0; r < C.nrange; r++) {
+                const uint64_t i = starts[r];
+                C.rstart[r] = (uint32_t)i;
+                const bool b1 = i < n && i + h1 >= n, b0 = i < n && i + h0 >= n, b0h = i + h1 < n && i + h1 + h0 >= n;
+                for (int v = 0; v < 2; v++) {
+                    const Scalar c1 = r1[2 * v + (b1 ? 1 : 0)];
+                    const Scalar c2 = rho0[2 * v + (b0 ? 1 : 0)];
+                    const Scalar c3 = c1 * rho0[2 * v + (b0h ? 1 : 0)];
+                    radix16_digits(c1, C.dig[v][r][0]);
+                    radix16_digits(c2, C.dig[v][r][1]);
+                    radix16_digits(c3, C.dig[v][r][2]);
+                }
+            }
+            int pf = ws.prof_begin("ipp_comb_fold", 2.0 * h1 * (4 * 64 + 64));
+            launch_ipp_comb_fold(C, ws.comb_stage, st);
+            ws.prof_end(pf);
+            Gh = ws.Gp[1].p; Hh = ws.Hp[1].p;
+            gfmt = MSM_CACHED;
+        } else if (h > 1) {
             PtD *Gn = as<PtD>(ws.Gp[k & 1]), *Hn = as<PtD>(ws.Hp[k & 1]);
             int pf = ws.prof_begin("ipp_fold_points", 6.0 * h * 64);
-            launch_ipp_fold_points(Gh, Hh, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn, ws.fold_stage, st);
+            launch_ipp_fold_points(Gh, Hh, gfmt, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
+                                   ws.fold_stage, st);
             ws.prof_end(pf);
             Gh = Gn; Hh = Hn;
+            gfmt = MSM_CACHED;
         }
         lam = lam * uinv;
         mu = mu * uk;
@@ -846,7 +970,7 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
         memcpy(comp.data() + (8 + m + k) * (size_t)32, ipp + 64 * k, 32);
         memcpy(comp.data() + (8 + m + lgn + k) * (size_t)32, ipp + 64 * k + 32, 32);
     }
-    ws.pts.grow((size_t)ns * sizeof(PtD) + 64);
+    ws.pts.grow((size_t)ns * sizeof(NielsD) + 64);
     ws.okflag.grow(64);
     ws.mscal.grow((size_t)ns * 32 + (size_t)ns * sizeof(ScD) + 64);
     uint32_t *compd = as<uint32_t>(ws.mscal);
@@ -854,7 +978,7 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
     BPG_HIP(hipMemcpyAsync(compd, comp.data(), comp.size(), hipMemcpyHostToDevice, st));
     int one = 1;
     BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
-    launch_decompress(compd, as<PtD>(ws.pts), as<int>(ws.okflag), ns, st);
+    launch_decompress(compd, as<NielsD>(ws.pts), as<int>(ws.okflag), ns, st);
     int ok = 0;
     BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, st));
     ws.sync();
@@ -868,8 +992,8 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
     for (int i = 0; i < 5; i++) ss[3 + m + i] = to_dev(Ts[i]);
     for (uint32_t k = 0; k < lgn; k++) { ss[8 + m + k] = to_dev(u2[k]); ss[8 + m + lgn + k] = to_dev(ui2[k]); }
     BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
-    MsmSeg seg[3] = {{as<ScD>(ws.gh), ctx.G, N, 0}, {as<ScD>(ws.gh) + N, ctx.H, N, 0}, {sscal, as<PtD>(ws.pts), ns, 0}};
-    MsmPlan pl = ws.msm->enqueue(seg, 3, 1, ws.rows_host);
+    MsmSeg seg[3] = {{as<ScD>(ws.gh), ctx.G, N, 0}, {as<ScD>(ws.gh) + N, ctx.H, N, 0}, {sscal, ws.pts.p, ns, 0}};
+    MsmPlan pl = ws.msm->enqueue(seg, 3, 1, ws.rows_host, MSM_NIELS);
     ws.sync();
     Point R;
     combine_rows(R, ws.rows_host, pl.W, pl.c);

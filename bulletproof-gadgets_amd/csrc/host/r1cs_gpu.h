@@ -23,16 +23,32 @@ using dev::ScD;
 // Per-device state shared by all threads: generator cache in HBM
 // (BulletproofGens::new(N,1) is circuit-independent, so derive once) and the
 // fixed-base tables of PedersenGens.
+// Comb tables of the generators for the IPP's first two rounds:
+// j in [N/4, N) of G and of H, 512 packed affine-Niels entries each.
+struct CombTables {
+    int device = 0;
+    uint32_t N = 0;
+    void *tabG = nullptr, *tabH = nullptr;
+    size_t bytes = 0;
+    ~CombTables();
+};
 struct DeviceContext {
     int device = 0;
     std::mutex mu;
     uint32_t gens_cap = 0;
-    PtD *G = nullptr, *H = nullptr;     // gens_cap points each
+    dev::NielsD *G = nullptr, *H = nullptr;   // gens_cap points each, affine Niels
     PtD *tabB = nullptr, *tabBb = nullptr;
     PtD *Bb = nullptr;                  // B_blinding as a device point
+    std::shared_ptr<CombTables> comb;   // for one N at a time
     static DeviceContext &get(int device);
     void ensure_gens(uint32_t N);       // thread-safe; grows the cache
+    // Tables for circuits of padded size N, built on first use; null when
+    // disabled (bpg_set_fold_tables / BPG_FOLD_TABLES=0), N < 8, or when they
+    // would not fit in free HBM with room left for workspaces.
+    std::shared_ptr<CombTables> ensure_comb(uint32_t N);
 };
+// -1 auto (env BPG_FOLD_TABLES, default on), 0 off, 1 on
+void set_fold_tables(int mode);
 
 // Flattened circuit resident on the device (inputs in HBM before timing).
 struct PreparedCS {

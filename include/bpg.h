@@ -80,6 +80,13 @@ void bpg_clear_seed(void);
 /* Added: select the HIP device used by the calling thread (default 0). */
 int bpg_set_device(int device);
 
+/* Added: IPP fold strategy (process-wide). mode 1: comb tables of the
+ * generators (HBM-resident, ~74 KB x N per device) fold rounds 0-1 in one
+ * table pass; mode 0: per-round variable-base fold; -1: automatic (tables
+ * when they fit in free HBM; env BPG_FOLD_TABLES=0 disables). Proof bytes are
+ * identical either way. */
+int bpg_set_fold_tables(int mode);
+
 /* ------------------------------------------------------------------------ */
 /* 2. Inner operator ABI: the flattened constraint system                     */
 /* ------------------------------------------------------------------------ */

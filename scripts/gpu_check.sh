@@ -1,10 +1,19 @@
 #!/bin/bash
-# GPU-box check: parity tests, bench line, rocprofv3 kernel stats.
+# GPU-box check: microbenchmarks (optional), parity tests, bench line,
+# rocprofv3 kernel stats. Every GPU step has its own time limit; the first
+# failure ends the script.
 set -e
 mkdir -p gpurun_out
 R=${ROUND:-r01}
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/${R}_gpu_tests.log 2>&1
-timeout -k 10 600 python bench.py > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err
+if [ "${MICRO:-0}" = 1 ]; then
+  (cd bulletproof-gadgets_amd && timeout -k 10 120 bin/comb_bench && timeout -k 10 120 bin/fold_bench_w2) > gpurun_out/${R}_micro.log 2>&1
+fi
+if [ "${TESTS:-1}" = 1 ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/${R}_gpu_tests.log 2>&1
+fi
+if [ "${BENCH:-1}" = 1 ]; then
+  timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err
+fi
 if [ "${PROF:-1}" = 1 ]; then
   ROOTD=$(pwd)
   cd /tmp && export TMPDIR=/tmp

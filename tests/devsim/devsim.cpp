@@ -34,7 +34,17 @@ int sim_pt_op(int op, const uint32_t *a, const uint32_t *b, uint32_t *r) {
         case 2: ge_add_c(s, p, qc); break;
         case 3: ge_sub_c(s, p, qc); break;
         case 4: ge_dbl(s, p); break;
-        default: { ge t; ge_dbl_t<false>(t, p); ge_dbl(t, t); ge_add_c(s, t, qc); break; }
+        case 5: { ge t; ge_dbl_t<false>(t, p); ge_dbl(t, t); ge_add_c(s, t, qc); break; }
+        case 6: case 7: {   // affine Niels madd / msub, operand through the packed 96-B table form
+            gen qn; ge_to_niels(qn, q);
+            uint4 pk[6]; genp_store(pk, qn);
+            gen qu; genp_unpack(qu, pk);
+            gen_cneg(qu, op == 7);
+            ge_madd(s, p, qu); break;
+        }
+        default: {          // Niels -> cached (2Z = 2) path of the fold kernel
+            gen qn; ge_to_niels(qn, q); gec c2; gen_to_cached(c2, qn); ge_add_c(s, p, c2); break;
+        }
     }
     ristretto_encode(r, s);
     return 0;

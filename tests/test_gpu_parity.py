@@ -110,6 +110,27 @@ def test_fixture_bit_exact(bpg, resources, name):
     assert S.verify_statement(name.encode(), fx["inst"], proof, coms, fx["gadgets"])
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("name", ["bounds_check", "less_than", "example", "inequality", "or5"])
+def test_fold_strategy_bit_exact(bpg, resources, name, mode):
+    """Both IPP fold strategies (per-round variable-base fold; comb-table pass
+    for rounds 0-1 with a lazily expanded round-1 MSM) give the oracle's bytes.
+    The fixtures put n - N/2 on both sides of N/4, so every lane class of the
+    table pass occurs."""
+    fx = read_fixture(os.path.join(resources, name))
+    seed = 900 + len(name)
+    lib = bpg.lib()
+    assert lib.bpg_set_fold_tables(mode) == 0
+    try:
+        bpg.set_seed(seed)
+        proof, coms = bpg.prove(name, fx["inst"], fx["wtns"], fx["gadgets"])
+    finally:
+        lib.bpg_set_fold_tables(-1)
+    o_proof, o_coms, _ = S.prove_statement(name.encode(), fx["inst"], fx["wtns"], fx["gadgets"], seed)
+    assert coms == o_coms
+    assert proof == o_proof
+
+
 @pytest.mark.parametrize("name", ["bounds_check", "less_than", "example"])
 def test_fixture_rejects(bpg, resources, name):
     fx = read_fixture(os.path.join(resources, name))
