@@ -43,6 +43,27 @@ def parse():
     return ap.parse_args()
 
 
+# single kernels bracketed live (bpg name -> rocprofv3 kernel name)
+KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1>", "msm_pass1_cached": "k_rbk_pass<true, 0>",
+           "ipp_fold_points": "k_ipp_fold_points<gec>",
+           "ipp_comb_fold": "k_ipp_comb_fold", "flatten": "k_flatten_short"}
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+FEMUL_PEAK_G = 263.5         # GF(2^255-19) multiplies/s x1e9, measured (profiles/*_micro.log, fe_variants V2)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/*_pmc.json, scripts/pmc_summary.py: FETCH_SIZE x 2 per
+    the gfx950 correction + WRITE_SIZE, separate passes), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k["hbm_bytes_per_launch"]
+
+
 def cpu_baseline(bpg, leaves):
     """The CPU oracle (oracle/, a C restatement of dalek/bulletproofs with
     dalek's algorithms, single thread) proving a bounded sample of the same
@@ -87,10 +108,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     import workloads as W
     bpg = W._bpg()
+    sys.path.insert(0, os.path.join(ROOT, "bulletproof-gadgets_amd"))
+    import dist as D
     bpg.lib().bpg_set_device(dev)
     ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
     threads = a.threads or max(1, min(16, ncpu // max(world, 1) if world > 1 else ncpu))
-    threads = min(threads, 16)
+    threads = min(threads, 64)
     batch = a.batch or 8 * threads
 
     inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * rank)
@@ -126,9 +149,7 @@ def main():
     dt = time.perf_counter() - t0
     L.bpg_profile_enable(0)
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = D.max_over_ranks(dt)
 
     # single-proof latency (one host thread), outside the timed region
     t1 = time.perf_counter()
@@ -141,24 +162,37 @@ def main():
     if not ok:
         raise SystemExit("bench: a timed proof failed to verify")
 
-    # roofline of the dominant kernel (live HIP-event timing inside the timed region)
-    stats = {}
-    for name in ("ipp_fold_points", "msm_ipp", "msm_commit", "flatten"):
-        lc, ms, by = ctypes.c_uint64(0), ctypes.c_double(0), ctypes.c_double(0)
+    # roofline of the dominant kernel (live HIP-event timing of single kernel
+    # launches inside the timed region, on the stream they run on)
+    def stat(name):
+        lc, ms, by, fm = ctypes.c_uint64(0), ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
         L.bpg_kernel_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
-        if L.bpg_kernel_stats(name.encode(), ctypes.byref(lc), ctypes.byref(ms), ctypes.byref(by)) == 0:
-            stats[name] = (lc.value, ms.value, by.value)
-    dom = max(stats, key=lambda k: stats[k][1]) if stats else None
+        L.bpg_kernel_femul.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
+        if L.bpg_kernel_stats(name.encode(), ctypes.byref(lc), ctypes.byref(ms), ctypes.byref(by)) != 0:
+            return None
+        L.bpg_kernel_femul(name.encode(), ctypes.byref(fm))
+        return lc.value, ms.value, by.value, fm.value
+    kernels = {k: stat(k) for k in KERNELS}
+    kernels = {k: v for k, v in kernels.items() if v}
+    jobs = {k: stat(k) for k in ("msm_commit", "msm_ipp")}
+    dom = max(kernels, key=lambda k: kernels[k][1]) if kernels else None
     roof = None
     if dom:
-        lc, ms, by = stats[dom]
-        achieved = (by / lc) / (ms / lc / 1e3) / 1e9  # GB/s per launch
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(achieved / 8000.0, 6), "traffic": None,
-                "launches": lc, "avg_launch_ms": round(ms / lc, 4),
+        lc, ms, by, fm = kernels[dom]
+        sec = ms / lc / 1e3                      # average launch duration
+        achieved = (by / lc) / sec / 1e9         # GB/s of algorithmic bytes
+        pmc = pmc_traffic(KERNELS[dom])
+        roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm", "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": pmc, "launches": lc, "avg_launch_ms": round(sec * 1e3, 4),
                 "alg_bytes_per_launch": round(by / lc, 1),
-                "device_ms_by_kernel": {k: round(v[1], 2) for k, v in stats.items()}}
+                # the kernels are VALU-bound (255-bit field arithmetic): the same
+                # launches against the measured GF(p) multiply peak
+                "valu": {"unit": "G fe_mul/s", "achieved": round(fm / lc / sec / 1e9, 2), "peak": FEMUL_PEAK_G,
+                         "frac": round(fm / lc / sec / 1e9 / FEMUL_PEAK_G, 4)},
+                "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
+                "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items() if v}}
 
     total_proofs = a.steps * batch * world
     value = total_proofs * q / dt

@@ -25,7 +25,8 @@ EXPORTS = [
     "bpg_prove_batch", "bpg_last_timings", "bpg_msm", "bpg_synthesize", "bpg_synthesize_verifier",
     "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free", "bpg_mimc_hash",
     "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
-    "bpg_rng_rate", "bpg_set_fold_tables",
+    "bpg_rng_rate", "bpg_set_fold_tables", "bpg_r1cs_verify_shard", "bpg_point_sum",
+    "bpg_kernel_femul",
 ]
 
 
@@ -73,6 +74,9 @@ def lib():
         L.bpg_pedersen_commit.argtypes = [vp, vp, vp, u32, vp]
         L.bpg_r1cs_prove.argtypes = [vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz), vp]
         L.bpg_r1cs_verify.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp]
+        L.bpg_r1cs_verify_shard.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, u32, u32, vp]
+        L.bpg_point_sum.argtypes = [vp, u32, vp]
+        L.bpg_set_fold_tables.argtypes = [ctypes.c_int]
         L.bpg_prepare.restype = vp
         L.bpg_prepare.argtypes = [vp, vp]
         L.bpg_prepared_free.argtypes = [vp]
@@ -217,6 +221,16 @@ class Context:
             raise BpgError(last_error())
         return rc == 1
 
+    def r1cs_verify_shard(self, label, view, V, proof, shard, nshards, entropy=b"\x05" * 32):
+        """-> (ok, partial): one shard of the verifier's mega-MSM (bpg.h)."""
+        Vb = b"".join(V) or b"\0" * 32
+        part = ctypes.create_string_buffer(32)
+        rc = lib().bpg_r1cs_verify_shard(self.h, label, len(label), ctypes.addressof(view), Vb, proof, len(proof),
+                                         entropy, shard, nshards, part)
+        if rc < 0:
+            raise BpgError(last_error())
+        return rc == 1, part.raw
+
     def prepare(self, view):
         p = lib().bpg_prepare(self.h, ctypes.addressof(view))
         if not p:
@@ -249,6 +263,15 @@ class Prepared:
             lib().bpg_prepared_free(self.h)
         except Exception:
             pass
+
+
+def point_sum(points):
+    """Sum of compressed Ristretto points (host code, no device needed)."""
+    buf = b"".join(points)
+    out = ctypes.create_string_buffer(32)
+    if lib().bpg_point_sum(buf, len(points), out) != 0:
+        raise BpgError(last_error() or "invalid point encoding")
+    return out.raw
 
 
 def last_timings():

@@ -15,6 +15,8 @@ struct ScD { uint32_t v[8]; };
 struct PtD { uint32_t v[40]; };
 // affine Niels (y+x, y-x, 2dxy), Z = 1: 3 x 10 limbs + 2 pad words = 128 B
 struct NielsD { uint32_t v[32]; };
+// affine (x, y), canonical words: 64 B
+struct AffD { uint32_t v[16]; };
 
 #define BPG_HIP(x)                                                                 \
     do {                                                                           \
@@ -29,6 +31,18 @@ struct HipError {
     HipError(hipError_t e, const char *x, const char *f, int l) : err(e), expr(x), file(f), line(l) {}
 };
 
+// Live kernel timing (bench.py roofline): the calling thread's sink brackets
+// single kernel launches with HIP events on their stream.
+struct ProfSink {
+    // alg_bytes: algorithmic HBM bytes of the launch; femul:
+    // GF(p) multiplications it performs (squarings counted as multiplies)
+    virtual int begin(const char *name, double alg_bytes, double femul) = 0;   // < 0: not recording
+    virtual void end(int handle) = 0;
+    virtual ~ProfSink() {}
+};
+void set_prof_sink(ProfSink *s);   // thread-local
+ProfSink *prof_sink();
+
 // -------------------------------------------------------------- points
 // Generators and decompressed inputs live in HBM as affine Niels points
 // (128 B, one line per random gather); folded generators are cached points
@@ -41,10 +55,14 @@ void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tab
 void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st);     // cached in
 void launch_compress(const NielsD *in, uint32_t *out, uint32_t count, hipStream_t st);  // Niels in
 void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count, hipStream_t st);
+void launch_decompress(const uint32_t *in, AffD *out, int *ok, uint32_t count, hipStream_t st);
+// affine copies of Niels points (MSM bases: half the gather bytes)
+void launch_to_affine(const NielsD *in, AffD *out, uint32_t count, hipStream_t st);
 
 // -------------------------------------------------------------- MSM
 #define MSM_CACHED 0   // bases are cached points (PtD)
 #define MSM_NIELS 1    // bases are affine Niels points (NielsD)
+#define MSM_AFFINE 2   // bases are affine (x, y) points (AffD, 64 B)
 struct MsmSeg {
     const ScD *scal;   // canonical scalars (< l)
     const void *base;  // PtD (cached) or NielsD, per the job's format
@@ -79,7 +97,7 @@ class MsmEngine {
   private:
     void reserve(const MsmPlan &p);
     hipStream_t st_;
-    DBuf keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_, cnt_, off_, E_, rk_a_, rk_b_, rp_a_, rp_b_, buckets_,
+    DBuf keys_, vals_, keys2_, vals2_, sort_tmp_, rk_a_, rk_b_, rp_a_, rp_b_, buckets_,
         bflag_, segacc_, rows_dev_;
 };
 

@@ -6,10 +6,13 @@
 //                       generators.rs BulletproofGens/PedersenGens
 //   curve25519-dalek@3.2.0  Straus/Pippenger MSM, Ristretto encode/decode
 // Design (MI355X-first, not a port): one thread per point/scalar lane,
-// 64-wide waves, sort-based signed-window Pippenger (hipcub radix sort +
-// fixed-chunk reduce-by-key passes, no 128-byte atomics), Montgomery scalar
+// 64-wide waves, sort-based signed-window Pippenger (look-back-free radix
+// sort + fixed-chunk reduce-by-key passes, no point atomics), Montgomery scalar
 // vectors, and a weighted single-scalar IPP point fold.
-#include <hipcub/hipcub.hpp>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "dev_field.h"
 #include "kernels.h"
@@ -31,6 +34,17 @@ static_assert(sizeof(NielsD) == sizeof(gen) && sizeof(gen) == 128, "niels layout
 #define AS_CGEN(p) reinterpret_cast<const gen *>(p)
 
 static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+static thread_local ProfSink *tl_sink = nullptr;
+void set_prof_sink(ProfSink *s) { tl_sink = s; }
+ProfSink *prof_sink() { return tl_sink; }
+struct ProfScope {   // brackets the launches issued while it lives
+    int h = -1;
+    ProfScope(const char *name, double bytes, double femul) {
+        if (tl_sink && name) h = tl_sink->begin(name, bytes, femul);
+    }
+    ~ProfScope() { if (tl_sink && h >= 0) tl_sink->end(h); }
+};
 
 // ===========================================================================
 // point kernels
@@ -151,18 +165,62 @@ void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count,
     BPG_HIP(hipGetLastError());
 }
 
+DEVI void store_affine(gaf *out, const fe &x, const fe &y) {
+    uint32_t w[16];
+    fe_tow(w, x); fe_tow(w + 8, y);
+    uint4 *d = reinterpret_cast<uint4 *>(out);
+#pragma unroll
+    for (int i = 0; i < 4; i++) d[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+__global__ __launch_bounds__(64) void k_decompress_aff(const uint32_t *__restrict__ in, gaf *__restrict__ out, int *ok,
+                                                        uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = in[8 * (size_t)i + k];
+    ge p;
+    if (!ristretto_decode(p, w)) { ge_identity(p); atomicAnd(ok, 0); }
+    store_affine(out + i, p.X, p.Y);     // decoded points have Z = 1
+}
+void launch_decompress(const uint32_t *in, AffD *out, int *ok, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_decompress_aff, dim3(nblk(count, 64)), dim3(64), 0, st, in, reinterpret_cast<gaf *>(out), ok,
+                       count);
+    BPG_HIP(hipGetLastError());
+}
+// (y+x, y-x) -> (x, y): x = (YpX - YmX) / 2, y = (YpX + YmX) / 2
+__global__ __launch_bounds__(64) void k_to_affine(const gen *__restrict__ in, gaf *__restrict__ out, uint32_t count) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    gen q;
+    gen_load(q, in + i);
+    fe inv2 = fe_from_words(0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                            0xffffffffu, 0x3fffffffu);   // (p + 1) / 2
+    fe x, y;
+    fe_sub(x, q.YpX, q.YmX); fe_mul(x, x, inv2);
+    fe_add(y, q.YpX, q.YmX); fe_mul(y, y, inv2);
+    store_affine(out + i, x, y);
+}
+void launch_to_affine(const NielsD *in, AffD *out, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_to_affine, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(in), reinterpret_cast<gaf *>(out),
+                       count);
+    BPG_HIP(hipGetLastError());
+}
+
 // ===========================================================================
 // Pippenger MSM
 //
-// Bases are cached points. One job = up to 8 (scalar, base) segments feeding
-// up to 2 MSMs. Signed c-bit windows give W digits per scalar; an entry
+// Bases are affine Niels (generators, decompressed points) or cached points
+// (folded generators), one format per job. One job = up to 12 (scalar, base)
+// segments feeding up to 2 MSMs. Signed c-bit windows give W digits per scalar; an entry
 // (key = row * half + |d| - 1, val = point | sign) per nonzero digit is
-// radix-sorted by key (hipcub), so each bucket is a contiguous run. Runs are
+// radix-sorted by key (k_rs_*), so each bucket is a contiguous run. Runs are
 // summed by fixed chunks of RBK_T entries per thread with keys/vals staged
 // through LDS (coalesced); a run that lies wholly inside one thread's chunk
-// goes straight to its bucket, runs that straddle chunks leave one partial
-// per chunk, which the next pass reduces the same way (pieces are sorted by
-// key). Buckets then fold into window rows (running sums per segment of
+// goes straight to its bucket, runs that straddle chunks leave pieces in
+// two fixed slots per chunk, which the next pass reduces the same way. Buckets then fold into window rows (running sums per segment of
 // buckets + a weighted correction, then a block reduction per row); the host
 // combines rows with c doublings each.
 // ===========================================================================
@@ -215,8 +273,154 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t ha
     }
 }
 
-// Stage one chunk of keys (and vals) into LDS with one pad word per RBK_T so
-// that thread t's entries t*T..t*T+T-1 sit at t*(T+1)+i (conflict-free).
+// ---------------------------------------------------------------------------
+// LSD radix sort of (key, value) pairs, 7-bit digits, written for sharing the
+// chip with other streams: per-block histograms, one single-workgroup scan,
+// then a stable per-block scatter — no decoupled look-back, so no block ever
+// spins waiting for a block that other streams' kernels keep off the CUs.
+// Stable ranking inside a wave: 7 ballots give each lane the mask of lanes
+// holding its digit; rank = popcount of that mask below the lane.
+// ---------------------------------------------------------------------------
+#define RS_BITS 7
+#define RS_BINS 128
+#define RS_BLOCK 256
+#define RS_ROUNDS 8
+#define RS_ITER (RS_BLOCK * RS_ROUNDS)
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict__ keys, uint32_t E, int shift,
+                                                      uint32_t tile, uint32_t nb, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[RS_BINS];
+    if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * tile, t1 = (t0 + tile < E) ? t0 + tile : E;
+    for (uint64_t i = t0 + threadIdx.x; i < t1; i += RS_BLOCK) atomicAdd(&h[(keys[i] >> shift) & (RS_BINS - 1)], 1u);
+    __syncthreads();
+    if (threadIdx.x < RS_BINS) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+// per digit d (one block each): exclusive scan of hist[d][0..nb) in place,
+// total[d] = the digit's count
+__global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist, uint32_t nb,
+                                                    uint32_t *__restrict__ total) {
+    __shared__ uint32_t sm[256];
+    const uint32_t t = threadIdx.x;
+    uint32_t *h = hist + (size_t)blockIdx.x * nb;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < nb; r0 += 256) {
+        const uint32_t i = r0 + t;
+        const uint32_t v = i < nb ? h[i] : 0u;
+        sm[t] = v;
+        __syncthreads();
+        for (uint32_t d = 1; d < 256; d <<= 1) {
+            const uint32_t a = t >= d ? sm[t - d] : 0u;
+            __syncthreads();
+            sm[t] += a;
+            __syncthreads();
+        }
+        if (i < nb) h[i] = carry + sm[t] - v;
+        carry += sm[255];
+        __syncthreads();
+    }
+    if (t == 0) total[blockIdx.x] = carry;
+}
+// Stable scatter of one block's tile, 2048 keys per iteration: wave ballots
+// rank keys within their digit, the iteration is reordered by digit in LDS,
+// then written out so that lanes with consecutive LDS slots of one digit
+// write consecutive addresses.
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                         uint32_t E, int shift, uint32_t tile, uint32_t nb,
+                                                         const uint32_t *__restrict__ hist,
+                                                         const uint32_t *__restrict__ total,
+                                                         uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+    __shared__ uint32_t base[RS_BINS], lstart[RS_BINS], tot[RS_BINS];
+    __shared__ uint32_t cnt[RS_ROUNDS][RS_BLOCK / 64][RS_BINS];
+    __shared__ uint32_t lk[RS_ITER], lv[RS_ITER];
+    const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull);
+    // digit offsets: exclusive scan of the digit totals, plus this block's column offset
+    if (t < RS_BINS) lstart[t] = total[t];
+    __syncthreads();
+    for (uint32_t d = 1; d < RS_BINS; d <<= 1) {
+        uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
+        __syncthreads();
+        if (t < RS_BINS) lstart[t] += a;
+        __syncthreads();
+    }
+    if (t < RS_BINS) base[t] = lstart[t] - total[t] + hist[t * nb + blockIdx.x];
+    const uint64_t t0 = (uint64_t)blockIdx.x * tile, t1 = (t0 + tile < E) ? t0 + tile : E;
+    for (uint64_t it = t0; it < t1; it += RS_ITER) {
+        uint32_t *cz = &cnt[0][0][0];
+        for (uint32_t j = t; j < RS_ROUNDS * (RS_BLOCK / 64) * RS_BINS; j += RS_BLOCK) cz[j] = 0;
+        __syncthreads();
+        uint32_t kk[RS_ROUNDS], vv[RS_ROUNDS], dd[RS_ROUNDS], rk[RS_ROUNDS];
+#pragma unroll
+        for (int r = 0; r < RS_ROUNDS; r++) {
+            const uint64_t idx = it + (uint64_t)r * RS_BLOCK + t;
+            const bool ok = idx < t1;
+            kk[r] = ok ? kin[idx] : 0u;
+            vv[r] = ok ? vin[idx] : 0u;
+            const uint32_t d = (kk[r] >> shift) & (RS_BINS - 1);
+            dd[r] = ok ? d : 0xffffffffu;
+            uint64_t m = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < RS_BITS; b++) {
+                const uint64_t bb = __ballot(ok && ((d >> b) & 1));
+                m &= ((d >> b) & 1) ? bb : ~bb;
+            }
+            rk[r] = (uint32_t)__popcll(m & below);
+            if (ok && rk[r] == 0) cnt[r][wave][d] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        if (t < RS_BINS) {   // offsets within the iteration, (round, wave) order
+            uint32_t run = 0;
+            for (int r = 0; r < RS_ROUNDS; r++)
+                for (int w = 0; w < RS_BLOCK / 64; w++) { const uint32_t c = cnt[r][w][t]; cnt[r][w][t] = run; run += c; }
+            tot[t] = run;
+            lstart[t] = run;
+        }
+        __syncthreads();
+        for (uint32_t d = 1; d < RS_BINS; d <<= 1) {   // inclusive scan of tot -> exclusive starts
+            uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
+            __syncthreads();
+            if (t < RS_BINS) lstart[t] += a;
+            __syncthreads();
+        }
+        if (t < RS_BINS) lstart[t] -= tot[t];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RS_ROUNDS; r++) {
+            if (dd[r] != 0xffffffffu) {
+                const uint32_t pos = lstart[dd[r]] + cnt[r][wave][dd[r]] + rk[r];
+                lk[pos] = kk[r];
+                lv[pos] = vv[r];
+            }
+        }
+        __syncthreads();
+        const uint32_t n_it = (uint32_t)((t1 - it) < RS_ITER ? (t1 - it) : RS_ITER);
+        for (uint32_t i = t; i < n_it; i += RS_BLOCK) {
+            const uint32_t key = lk[i];
+            const uint32_t d = (key >> shift) & (RS_BINS - 1);
+            const uint32_t g = base[d] + (i - lstart[d]);
+            kout[g] = key;
+            vout[g] = lv[i];
+        }
+        __syncthreads();
+        if (t < RS_BINS) base[t] += tot[t];
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Run reduction over the sorted entries, by fixed chunks of RBK_T entries per
+// thread (keys/values staged through LDS with one pad word per RBK_T, so
+// thread t's entries t*T..t*T+T-1 sit at t*(T+1)+i, conflict-free). A run
+// wholly inside one chunk goes straight to its bucket. Every chunk writes
+// exactly two slots for the next pass — the piece of a run that began before
+// it (head) and of one that continues after it (tail) — and a filler (key |
+// RBK_FILL, no point) where it has none, so the next pass's input is still
+// sorted and its size is known on the host: no count, no scan, one launch
+// per pass. A run made only of fillers writes nothing.
+// ---------------------------------------------------------------------------
+#define RBK_FILL 0x80000000u
+#define RBK_KEY(x) ((x) & 0x7fffffffu)
 DEVI uint32_t rbk_lds(uint32_t j) { return j + j / RBK_T; }
 DEVI void rbk_stage(uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t base, uint64_t E, uint32_t invalid) {
     for (uint32_t k = threadIdx.x; k < RBK_CHUNK; k += RBK_BLOCK) {
@@ -224,86 +428,39 @@ DEVI void rbk_stage(uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t ba
         sk[rbk_lds(k)] = idx < E ? keys[idx] : invalid;
     }
 }
-DEVI uint64_t rbk_E(uint64_t E_host, const uint32_t *E_dev) { return E_dev ? *E_dev : E_host; }
-// key of the global entries just before / after this thread's chunk
-DEVI uint32_t rbk_prev_key(const uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t gstart, uint32_t t,
-                           uint32_t invalid) {
-    if (gstart == 0) return invalid;
-    return t ? sk[rbk_lds(t * RBK_T - 1)] : keys[gstart - 1];
-}
-DEVI uint32_t rbk_next_key(const uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t gend, uint64_t E,
-                           uint32_t t, uint32_t invalid) {
-    if (gend >= E) return invalid;
-    return (t + 1 < RBK_BLOCK) ? sk[rbk_lds((t + 1) * RBK_T)] : keys[gend];
-}
-
-// pieces this thread leaves for the next pass (runs touching a chunk edge
-// that continue into a neighbour chunk)
-__global__ __launch_bounds__(RBK_BLOCK) void k_rbk_count(const uint32_t *__restrict__ keys, uint64_t E_host,
-                                                         const uint32_t *E_dev, uint32_t invalid,
-                                                         uint32_t *__restrict__ cnt) {
-    __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
-    const uint64_t E = rbk_E(E_host, E_dev);
-    const uint64_t base = (uint64_t)blockIdx.x * RBK_CHUNK;
-    const uint32_t t = threadIdx.x;
-    const uint32_t j = blockIdx.x * RBK_BLOCK + t;
-    if (base >= E) { cnt[j] = 0; return; }
-    rbk_stage(sk, keys, base, E, invalid);
-    __syncthreads();
-    const uint64_t gs = base + (uint64_t)t * RBK_T, ge_ = gs + RBK_T;
-    uint32_t c = 0;
-    if (gs < E) {
-        const uint32_t first = sk[rbk_lds(t * RBK_T)];
-        const uint32_t last = sk[rbk_lds(t * RBK_T + RBK_T - 1)];
-        const uint32_t pk = rbk_prev_key(sk, keys, gs, t, invalid);
-        const uint32_t nk = rbk_next_key(sk, keys, ge_, E, t, invalid);
-        if (first != invalid) {
-            const bool head_open = (pk == first), tail_open = (last != invalid) && (nk == last);
-            if (first == last) c = (head_open || tail_open) ? 1 : 0;
-            else c = (head_open ? 1 : 0) + (tail_open ? 1 : 0);
-        }
-    }
-    cnt[j] = c;
-}
-
-// acc += +-base[v]: one gather of a cached (160 B) or affine Niels (128 B,
-// one line, 7M madd) base, by the job's base format
+// Base gathers by the job's base format: cached (160 B) or affine Niels
+// (128 B, one line, 7M madd).
+template <int FMT> struct BaseOf { typedef gec T; };
+template <> struct BaseOf<MSM_NIELS> { typedef gen T; };
+template <> struct BaseOf<MSM_AFFINE> { typedef gaf T; };
 template <int FMT>
-DEVI void msm_add_base(ge &acc, const SegTab &T, uint32_t v) {
-    uint32_t g = v & 0x7fffffffu;
-    int si = seg_of(T, g);
-    if (FMT == MSM_NIELS) {
-        gen p;
-        gen_load(p, reinterpret_cast<const gen *>(T.base[si]) + (g - T.gofs[si]));
-        gen_cneg(p, v >> 31);
-        ge_madd(acc, acc, p);
-    } else {
-        gec p;
-        gec_load(p, reinterpret_cast<const gec *>(T.base[si]) + (g - T.gofs[si]));
-        gec_cneg(p, v >> 31);
-        ge_add_c(acc, acc, p);
-    }
+DEVI void msm_load_base(typename BaseOf<FMT>::T &p, const SegTab &T, uint32_t v) {
+    const uint32_t g = v & 0x7fffffffu;
+    const int si = seg_of(T, g);
+    pt_load(p, reinterpret_cast<const typename BaseOf<FMT>::T *>(T.base[si]) + (g - T.gofs[si]));
 }
-// Sum runs. FIRST: entries are (key, signed base index); else entries are
-// pieces (key, extended partial at the same index) from the previous pass.
+DEVI void msm_add_loaded(ge &acc, gen &p, bool neg) { gen_cneg(p, neg); ge_madd(acc, acc, p); }
+DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) { gec_cneg(p, neg); ge_add_c(acc, acc, p); }
+DEVI void msm_add_loaded(ge &acc, gaf &p, bool neg) {
+    gen q; gaf_to_niels(q, p);
+    if (neg) { fe t = q.YpX; q.YpX = q.YmX; q.YmX = t; fe_neg(q.T2d, q.T2d); }
+    ge_madd(acc, acc, q);
+}
+
+// FIRST: entries are (key, signed base index) and the gather of entry i+1 is
+// issued before entry i's addition; otherwise entries are slots (key or
+// key|RBK_FILL, extended point at the same index) of the previous pass.
 template <bool FIRST, int FMT>
-__global__ __launch_bounds__(RBK_BLOCK) void k_rbk_sum(const uint32_t *__restrict__ keys,
-                                                       const uint32_t *__restrict__ vals,
-                                                       const ge *__restrict__ pin, SegTab T, uint64_t E_host,
-                                                       const uint32_t *E_dev, uint32_t invalid,
-                                                       const uint32_t *__restrict__ off,
-                                                       const uint32_t *__restrict__ cnt, uint32_t nthr,
-                                                       uint32_t *__restrict__ E_out, uint32_t *__restrict__ kout,
-                                                       ge *__restrict__ pout, ge *__restrict__ buckets,
-                                                       uint8_t *__restrict__ bflag) {
+__global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restrict__ keys,
+                                                        const uint32_t *__restrict__ vals,
+                                                        const ge *__restrict__ pin, SegTab T, uint64_t E,
+                                                        uint32_t invalid, uint32_t *__restrict__ kout,
+                                                        ge *__restrict__ pout, ge *__restrict__ buckets,
+                                                        uint8_t *__restrict__ bflag) {
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
     __shared__ uint32_t sv[FIRST ? RBK_CHUNK + RBK_BLOCK : 1];
     const uint32_t t = threadIdx.x;
-    // pieces this pass leaves (the next pass's entry count)
-    if (blockIdx.x * RBK_BLOCK + t == nthr - 1) *E_out = off[nthr - 1] + cnt[nthr - 1];
-    const uint64_t E = rbk_E(E_host, E_dev);
     const uint64_t base = (uint64_t)blockIdx.x * RBK_CHUNK;
-    if (base >= E) return;
     rbk_stage(sk, keys, base, E, invalid);
     if (FIRST) {
         for (uint32_t k = t; k < RBK_CHUNK; k += RBK_BLOCK) {
@@ -312,55 +469,82 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_sum(const uint32_t *__restric
         }
     }
     __syncthreads();
+    const uint64_t c = (uint64_t)blockIdx.x * RBK_BLOCK + t;
+    uint32_t *ko = kout + 2 * c;
+    ge *po = pout + 2 * c;
     const uint64_t gs = base + (uint64_t)t * RBK_T;
-    if (gs >= E) return;
-    const uint32_t first = sk[rbk_lds(t * RBK_T)];
-    if (first == invalid) return;
-    const uint32_t pk = rbk_prev_key(sk, keys, gs, t, invalid);
-    const uint32_t nk = rbk_next_key(sk, keys, gs + RBK_T, E, t, invalid);
-    uint32_t o = off[blockIdx.x * RBK_BLOCK + t];
+    const uint32_t first = RBK_KEY(sk[rbk_lds(t * RBK_T)]);
+    if (gs >= E || first == invalid) { ko[0] = invalid; ko[1] = invalid; return; }
+    const uint32_t pk = gs == 0 ? invalid : RBK_KEY(t ? sk[rbk_lds(t * RBK_T - 1)] : keys[gs - 1]);
+    const uint64_t gn = gs + RBK_T;
+    const uint32_t nk = gn >= E ? invalid : RBK_KEY((t + 1 < RBK_BLOCK) ? sk[rbk_lds((t + 1) * RBK_T)] : keys[gn]);
+    const bool open_start = pk == first;
+    bool head_done = false, real = false;
     uint32_t cur = first;
-    bool open_start = (pk == first);     // the run being summed began in an earlier chunk
     ge acc;
     ge_identity(acc);
+    typename BaseOf<FMT>::T pnext;
+    if (FIRST) msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T)]);
     for (uint32_t i = 0; i < RBK_T; i++) {
-        const uint32_t k = sk[rbk_lds(t * RBK_T + i)];
+        const uint32_t x = sk[rbk_lds(t * RBK_T + i)];
+        const uint32_t k = RBK_KEY(x);
         if (k == invalid) break;
         if (k != cur) {
-            if (open_start) { kout[o] = cur; ge_store(pout + o, acc); o++; }
-            else { ge_store(buckets + cur, acc); bflag[cur] = 1; }
-            cur = k; open_start = false;
+            if (!head_done) {
+                if (open_start) { ko[0] = cur | (real ? 0u : RBK_FILL); if (real) ge_store(po, acc); }
+                else { if (real) { ge_store(buckets + cur, acc); bflag[cur] = 1; } ko[0] = cur | RBK_FILL; }
+                head_done = true;
+            } else if (real) {
+                ge_store(buckets + cur, acc); bflag[cur] = 1;
+            }
+            cur = k; real = false;
             ge_identity(acc);
         }
         if (FIRST) {
-            msm_add_base<FMT>(acc, T, sv[rbk_lds(t * RBK_T + i)]);
-        } else {
+            typename BaseOf<FMT>::T p = pnext;
+            const uint32_t v = sv[rbk_lds(t * RBK_T + i)];
+            if (i + 1 < RBK_T && RBK_KEY(sk[rbk_lds(t * RBK_T + i + 1)]) != invalid)
+                msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T + i + 1)]);
+            msm_add_loaded(acc, p, v >> 31);
+            real = true;
+        } else if (!(x & RBK_FILL)) {
             ge p; ge_load(p, pin + gs + i);
             ge_add(acc, acc, p);
+            real = true;
         }
     }
-    // the last run is open if the next chunk continues it
-    if (open_start || nk == cur) { kout[o] = cur; ge_store(pout + o, acc); }
-    else { ge_store(buckets + cur, acc); bflag[cur] = 1; }
+    const bool tail_open = nk == cur;
+    if (!head_done) {            // one run in the chunk
+        if (open_start || tail_open) { ko[0] = cur | (real ? 0u : RBK_FILL); if (real) ge_store(po, acc); }
+        else { if (real) { ge_store(buckets + cur, acc); bflag[cur] = 1; } ko[0] = cur | RBK_FILL; }
+        ko[1] = cur | RBK_FILL;
+    } else if (tail_open) {
+        ko[1] = cur | (real ? 0u : RBK_FILL);
+        if (real) ge_store(po + 1, acc);
+    } else {
+        if (real) { ge_store(buckets + cur, acc); bflag[cur] = 1; }
+        ko[1] = cur | RBK_FILL;
+    }
 }
-// After the last pass: a key may still have several pieces (giant runs);
-// the piece that starts the run sums the rest and owns the bucket.
+// After the last pass: the head slot of each run sums the run's real pieces
+// and owns the bucket (serial; long only for giant runs of structured digits).
 __global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
-                                                  const uint32_t *E_dev, uint64_t cap, ge *__restrict__ buckets,
+                                                  uint64_t E, uint32_t invalid, ge *__restrict__ buckets,
                                                   uint8_t *__restrict__ bflag) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t E = *E_dev;
-    if (i >= cap || i >= E) return;
-    uint32_t k = keys[i];
-    if (i > 0 && keys[i - 1] == k) return;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    const uint32_t k = RBK_KEY(keys[i]);
+    if (k == invalid || (i > 0 && RBK_KEY(keys[i - 1]) == k)) return;
     ge acc, p;
-    ge_load(acc, pts + i);
-    for (uint64_t j = i + 1; j < E && keys[j] == k; j++) {
+    ge_identity(acc);
+    bool real = false;
+    for (uint64_t j = i; j < E && RBK_KEY(keys[j]) == k; j++) {
+        if (keys[j] & RBK_FILL) continue;
         ge_load(p, pts + j);
         ge_add(acc, acc, p);
+        real = true;
     }
-    ge_store(buckets + k, acc);
-    bflag[k] = 1;
+    if (real) { ge_store(buckets + k, acc); bflag[k] = 1; }
 }
 // Window rows from buckets: R_row = sum_b (b+1) S_b over the half buckets.
 // Level 1 (thread per segment of L buckets): A_s = sum_j (j+1) S_{sL+j} and
@@ -391,24 +575,35 @@ DEVI void ge_dbl_n(ge &r, int n) {
     for (int i = 1; i < n; i++) ge_dbl_t<false>(r, r);
     if (n > 0) ge_dbl_t<true>(r, r);
 }
-// Level 2, one block per row. Thread t owns segments [tK, tK+K):
-//   sum_s s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t,
+// Level 2, ROW_SPLIT blocks per row; block j owns segments [s0, s0 + M)
+// (M = nseg / ROW_SPLIT) and thread t of it [s0 + tK, s0 + tK + K):
+//   sum_{s in block} s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t + s0 * sum_t run_t,
 //   sum_t t run_t = sum_{k>=1} suffix_k (suffix scan in LDS).
-// Each thread forms Q_t = A'_t + L * ((acc_t - run_t) + K * [t>=1] suffix_t);
-// a tree reduction of Q_t gives R. L and K are powers of two.
+// Block j writes P_j = sum A_s + L * (that); k_row_final sums the P_j of a
+// row. L, K and M are powers of two; s0 = j M.
+DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {   // k * p, k < 2^8
+    ge acc; ge_identity(acc);
+    for (int b = 7; b >= 0; b--) {
+        ge_dbl(acc, acc);
+        if ((k >> b) & 1) ge_add(acc, acc, p);
+    }
+    r = acc;
+}
 __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
-                                                    uint32_t nseg, int lgL, ge *__restrict__ rows_out) {
+                                                    uint32_t nseg, int lgL, uint32_t split,
+                                                    ge *__restrict__ parts) {
     __shared__ ge sh[256];
-    const uint32_t row = blockIdx.x, t = threadIdx.x;
-    const uint32_t K = (nseg + 255) / 256;
+    const uint32_t row = blockIdx.x / split, j = blockIdx.x % split, t = threadIdx.x;
+    const uint32_t M = nseg / split, s0 = j * M;
+    const uint32_t K = (M + 255) / 256;
     int lgK = 0;
     while ((1u << lgK) < K) lgK++;
-    const ge *A = segA + (size_t)row * nseg, *T = segT + (size_t)row * nseg;
+    const ge *A = segA + (size_t)row * nseg + s0, *T = segT + (size_t)row * nseg + s0;
     ge sumA, run, acc, p;
     ge_identity(sumA); ge_identity(run); ge_identity(acc);
-    for (int j = (int)K - 1; j >= 0; j--) {
-        uint32_t s = t * K + j;
-        if (s >= nseg) continue;
+    for (int k = (int)K - 1; k >= 0; k--) {
+        uint32_t s = t * K + k;
+        if (s >= M) continue;
         ge_load(p, A + s); ge_add(sumA, sumA, p);
         ge_load(p, T + s); ge_add(run, run, p);
         ge_add(acc, acc, run);
@@ -424,12 +619,21 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
         if (act) ge_store(&sh[t], a);
     }
     __syncthreads();
-    ge q, suf;
+    ge q, suf, tot;
     ge_load(suf, &sh[t]);
+    ge_load(tot, &sh[0]);                  // sum of run over the block
     if (t == 0) ge_identity(suf);
     ge_dbl_n(suf, lgK);                    // K * suffix_t
     ge_sub(q, acc, run);
     ge_add(q, q, suf);
+    if (t == 0 && j) {                     // + s0 * sum run, s0 = j * M
+        ge m;
+        int lgM = 0;
+        while ((1u << lgM) < M) lgM++;
+        ge_mul_small(m, tot, j);
+        ge_dbl_n(m, lgM);
+        ge_add(q, q, m);
+    }
     ge_dbl_n(q, lgL);                      // L * (...)
     ge_add(q, q, sumA);
     __syncthreads();
@@ -443,20 +647,30 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
             ge_store(&sh[t], a);
         }
     }
-    if (t == 0) { ge r; ge_load(r, &sh[0]); ge_store(rows_out + row, r); }
+    if (t == 0) { ge r; ge_load(r, &sh[0]); ge_store(parts + blockIdx.x, r); }
+}
+__global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ parts, uint32_t rows, uint32_t split,
+                                                  ge *__restrict__ rows_out) {
+    const uint32_t row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= rows) return;
+    ge acc, p;
+    ge_load(acc, parts + (size_t)row * split);
+    for (uint32_t j = 1; j < split; j++) { ge_load(p, parts + (size_t)row * split + j); ge_add(acc, acc, p); }
+    ge_store(rows_out + row, acc);
 }
 
 static int msm_window(uint64_t total) {
     int lg = 0;
     while ((1ULL << (lg + 1)) <= total) lg++;
-    int c = lg - 3;
+    static const int bias = [] { const char *e = getenv("BPG_MSM_C_BIAS"); return e ? atoi(e) : 3; }();
+    int c = lg - bias;
     if (c < 4) c = 4;
     if (c > 16) c = 16;
     return c;
 }
 
 MsmEngine::~MsmEngine() {
-    DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &scan_tmp_, &cnt_, &off_, &E_,
+    DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_,
                     &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &bflag_, &segacc_, &rows_dev_};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -474,22 +688,38 @@ void DBuf::grow(size_t need) {
 void MsmEngine::reserve(const MsmPlan &p) {
     size_t kb = p.E0 * 4;
     keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
-    sort_tmp_.grow(p.sort_tmp);
-    scan_tmp_.grow(p.scan_tmp);
-    uint64_t nthr = ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK + 1;
-    cnt_.grow(nthr * 4); off_.grow(nthr * 4);
-    E_.grow(64 * 4);
-    rk_a_.grow(p.capE * 4); rk_b_.grow(p.capE * 4);
-    rp_a_.grow(p.capE * sizeof(ge)); rp_b_.grow(p.capE * sizeof(ge));
+    sort_tmp_.grow((size_t)RS_BINS * 2049 * 4 + 256);       // radix-sort block histograms + totals
+    rk_a_.grow(p.capE * 4); rp_a_.grow(p.capE * sizeof(ge));
+    rk_b_.grow(p.capE * 4 / 4 + 1024); rp_b_.grow((p.capE / 4 + 256) * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
     bflag_.grow((size_t)p.rows * p.half);
     segacc_.grow((size_t)2 * p.rows * p.nseg_per_row * sizeof(ge));
     rows_dev_.grow((size_t)p.rows * sizeof(ge));
 }
 
+// sort (keys, vals) -> sorted pairs; returns which buffers hold them
+static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2, uint64_t E, int key_bits,
+                       uint32_t *hist, hipStream_t st) {
+    if (E < 2) return;
+    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (E + 4095) / 4096));
+    uint64_t tile = (E + nb - 1) / nb;
+    tile = (tile + RS_ITER - 1) / RS_ITER * RS_ITER;
+    uint32_t *total = hist + (size_t)RS_BINS * nb;
+    for (int shift = 0; shift < key_bits; shift += RS_BITS) {
+        hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_BLOCK), 0, st, k, (uint32_t)E, shift, (uint32_t)tile, nb, hist);
+        hipLaunchKernelGGL(k_rs_colscan, dim3(RS_BINS), dim3(256), 0, st, hist, nb, total);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_BLOCK), 0, st, k, v, (uint32_t)E, shift, (uint32_t)tile, nb,
+                           hist, total, k2, v2);
+        std::swap(k, k2);
+        std::swap(v, v2);
+    }
+    BPG_HIP(hipGetLastError());
+}
+
 MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt) {
     if (nseg < 1 || nseg > MSM_MAXSEG) throw HipError(hipErrorInvalidValue, "nseg", __FILE__, __LINE__);
-    if (fmt != MSM_NIELS && fmt != MSM_CACHED) throw HipError(hipErrorInvalidValue, "fmt", __FILE__, __LINE__);
+    if (fmt != MSM_NIELS && fmt != MSM_CACHED && fmt != MSM_AFFINE)
+        throw HipError(hipErrorInvalidValue, "fmt", __FILE__, __LINE__);
     MsmPlan p{};
     SegTab T{};
     uint64_t total = 0;
@@ -513,14 +743,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     uint32_t invalid = (uint32_t)D;
     p.key_bits = 1;
     while ((1ULL << p.key_bits) <= D) p.key_bits++;
-    // pieces after a pass: at most 2 per thread chunk
-    p.capE = std::min<uint64_t>(p.E0, 2 * ((p.E0 + RBK_T - 1) / RBK_T) + 2);
-    // passes: each leaves at most 2 pieces per 16-entry chunk, so runs of
-    // random-looking digits (<~100 entries) are whole after two; a giant run
-    // (structured scalars, e.g. all 0/1) still completes in k_rbk_final,
-    // whose run head sums the remaining pieces serially.
-    p.passes = 1;
-    { uint64_t r = RBK_T / 2; while (r < total + 1 && p.passes < 3) { r *= RBK_T / 2; p.passes++; } }
+    // slots after pass 1: two per thread chunk, padded to whole blocks
+    p.capE = 2 * ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
     p.seglen = p.half < 8 ? p.half : 8;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
@@ -530,16 +754,6 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         }
         return p;
     }
-    {
-        size_t s = 0;
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (int)p.E0, 0, (int)p.key_bits, st_);
-        p.sort_tmp = s;
-        size_t s2 = 0;
-        uint64_t nthr = ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
-        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nthr, st_);
-        p.scan_tmp = s2;
-    }
     reserve(p);
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     uint8_t *bflag = (uint8_t *)bflag_.p;
@@ -548,41 +762,42 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
                        (uint32_t)p.half, invalid, keys, vals);
     BPG_HIP(hipGetLastError());
-    size_t sbytes = p.sort_tmp;
-    BPG_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp_.p, sbytes, keys, keys2, vals, vals2, (int)p.E0, 0,
-                                               (int)p.key_bits, st_));
-    uint32_t *cnt = (uint32_t *)cnt_.p, *off = (uint32_t *)off_.p, *Ed = (uint32_t *)E_.p;
-    const uint32_t *kin = keys2;
+    radix_sort(keys, vals, keys2, vals2, p.E0, (int)p.key_bits, (uint32_t *)sort_tmp_.p, st_);
+    // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
+    uint64_t E = p.E0;
+    const uint32_t *kin = keys;
     const ge *pin = nullptr;
     uint32_t *kout = (uint32_t *)rk_a_.p;
     ge *pout = AS_GE(rp_a_.p);
-    uint64_t Ebound = p.E0;
-    const uint32_t *Ein = nullptr;
-    for (int pass = 0; pass < p.passes; pass++) {
-        uint32_t nblocks = (uint32_t)((Ebound + RBK_CHUNK - 1) / RBK_CHUNK);
-        if (nblocks == 0) nblocks = 1;
-        uint32_t nthr = nblocks * RBK_BLOCK;
-        hipLaunchKernelGGL(k_rbk_count, dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, Ebound, Ein, invalid, cnt);
-        size_t tb = p.scan_tmp;
-        BPG_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp_.p, tb, cnt, off, (int)nthr, st_));
-        if (pass == 0 && fmt == MSM_NIELS)
-            hipLaunchKernelGGL((k_rbk_sum<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
-                               (const uint32_t *)vals2, pin, T, Ebound, Ein, invalid, off, cnt, nthr, Ed + pass, kout, pout, buckets, bflag);
-        else if (pass == 0)
-            hipLaunchKernelGGL((k_rbk_sum<true, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
-                               (const uint32_t *)vals2, pin, T, Ebound, Ein, invalid, off, cnt, nthr, Ed + pass, kout, pout, buckets, bflag);
+    p.passes = 0;
+    for (;;) {
+        const uint32_t nblocks = (uint32_t)std::max<uint64_t>(1, (E + RBK_CHUNK - 1) / RBK_CHUNK);
+        // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
+        ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"), 96.0 * (double)total,
+                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);   // one mixed addition per entry
+        if (p.passes == 0 && fmt == MSM_NIELS)
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin, T,
+                               E, invalid, kout, pout, buckets, bflag);
+        else if (p.passes == 0 && fmt == MSM_AFFINE)
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_AFFINE>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
+                               T, E, invalid, kout, pout, buckets, bflag);
+        else if (p.passes == 0)
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
+                               T, E, invalid, kout, pout, buckets, bflag);
         else
-            hipLaunchKernelGGL((k_rbk_sum<false, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
-                               (const uint32_t *)vals2, pin, T, Ebound, Ein, invalid, off, cnt, nthr, Ed + pass, kout, pout, buckets, bflag);
+            hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
+                               T, E, invalid, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
-        Ein = Ed + pass;
-        Ebound = std::min<uint64_t>(Ebound, p.capE);
+        p.passes++;
+        E = 2 * (uint64_t)nblocks * RBK_BLOCK;
         kin = kout;
         pin = pout;
-        kout = (kout == (uint32_t *)rk_a_.p) ? (uint32_t *)rk_b_.p : (uint32_t *)rk_a_.p;
-        pout = (pout == AS_GE(rp_a_.p)) ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
+        if (E <= 8192 || p.passes >= 5) break;
+        const bool a = kout == (uint32_t *)rk_a_.p;
+        kout = a ? (uint32_t *)rk_b_.p : (uint32_t *)rk_a_.p;
+        pout = a ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
     }
-    hipLaunchKernelGGL(k_rbk_final, dim3(nblk(Ebound, 64)), dim3(64), 0, st_, kin, pin, Ein, Ebound, buckets, bflag);
+    hipLaunchKernelGGL(k_rbk_final, dim3(nblk(E, 64)), dim3(64), 0, st_, kin, pin, E, invalid, buckets, bflag);
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
     ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
     hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
@@ -590,7 +805,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     int lgL = 0;
     while ((1 << lgL) < p.seglen) lgL++;
     hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                       (uint32_t)p.nseg_per_row, lgL, AS_GE(rows_dev_.p));
+                       (uint32_t)p.nseg_per_row, lgL, 1u, AS_GE(rows_dev_.p));
     BPG_HIP(hipGetLastError());
     BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;
@@ -1072,6 +1287,16 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
     if (!blocks) return;
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldArgs), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
+    // reads P_L, P_R of G and H, writes G', H': 6 x 64 B per lane pair;
+    // per lane: doublings (3M+4S), digit additions (8M), odd multiples, final add
+    double fem = 0;
+    for (uint32_t k = 0; k < A.nseg; k++) {
+        const FoldSched &S = A.sc[A.sched[k]];
+        uint32_t dbl = S.tail;
+        for (uint32_t d = 1; d < S.ndig; d++) dbl += S.gap[d];
+        fem += (double)(A.end[k] - A.start[k]) * (7.0 * dbl + 8.0 * S.ndig + 40.0);
+    }
+    ProfScope ps("ipp_fold_points", 6.0 * h * 64, fem);
     if (in_fmt == MSM_NIELS)
         hipLaunchKernelGGL(k_ipp_fold_points<gen>, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
     else
@@ -1175,6 +1400,17 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombArgs), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
     const uint32_t nb = (args.h1 + 63) / 64;
+    // reads 4 level-0 points, writes 1 level-2 point per lane, G and H;
+    // one 7M madd per nonzero digit (+ the base term and the cached output)
+    double fem = 0;
+    for (uint32_t v = 0; v < 2; v++)
+        for (uint32_t r = 0; r < args.nrange; r++) {
+            const uint32_t lo = args.rstart[r], hi = r + 1 < args.nrange ? args.rstart[r + 1] : args.h1;
+            uint32_t nz = 0;
+            for (int t = 0; t < 3; t++) for (int w = 0; w < 64; w++) nz += args.dig[v][r][t][w] != 0;
+            fem += (double)(hi - lo) * (7.0 * (nz + 1) + 1.0);
+        }
+    ProfScope ps("ipp_comb_fold", 2.0 * args.h1 * (4 * 64 + 64), fem);
     hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, reinterpret_cast<const CombArgs *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }

@@ -182,6 +182,33 @@ int bpg_r1cs_verify(bpg_ctx *ctx, const uint8_t *label, size_t label_len, const 
     }, -1);
 }
 
+int bpg_r1cs_verify_shard(bpg_ctx *ctx, const uint8_t *label, size_t label_len, const bpg_r1cs_view *cs,
+                          const uint8_t *V, const uint8_t *proof, size_t proof_len, const uint8_t entropy[32],
+                          uint32_t shard, uint32_t nshards, uint8_t partial[32]) {
+    return guarded([&]() -> int {
+        if (nshards < 2) throw std::runtime_error("nshards must be >= 2 (use bpg_r1cs_verify)");
+        bpg_r1cs_view v = *cs;
+        v.a_L = v.a_R = v.a_O = v.v = v.v_blinding = nullptr;
+        std::unique_ptr<PreparedCS> P = prepare_cs(&v, ctx->device);
+        return gpu_verify_shard(*P, label, label_len, V, proof, proof_len, entropy, shard, nshards, partial);
+    }, -1);
+}
+
+// Host-only: sum of compressed Ristretto points (the verifier shards'
+// partials); the identity encodes as 32 zero bytes.
+int bpg_point_sum(const uint8_t *points, uint32_t count, uint8_t out[32]) {
+    return guarded([&]() -> int {
+        Point acc, p;
+        pt_identity(acc);
+        for (uint32_t i = 0; i < count; i++) {
+            if (!ristretto_decompress(p, points + 32 * (size_t)i)) return -1;
+            Point t; pt_add(t, acc, p); acc = t;
+        }
+        ristretto_compress(out, acc);
+        return 0;
+    }, -1);
+}
+
 struct bpg_prepared { std::unique_ptr<PreparedCS> p; };
 bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
     return guarded([&]() -> bpg_prepared * {
@@ -260,6 +287,10 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         // producers: ~half the threads (one lockstep group of 8 each); slots
         // (device buffers) for the groups being drawn plus a queue per consumer
         uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(groups, threads / 2));
+        if (const char *e = getenv("BPG_PRODUCERS")) {   // tuning override
+            int v = atoi(e);
+            if (v >= 1 && (uint32_t)v < threads) P = std::min<uint32_t>(groups, (uint32_t)v);
+        }
         uint32_t C = std::max<uint32_t>(1, std::min<uint32_t>(count, threads > P ? threads - P : 1));
         uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
         std::vector<uint8_t *> slot = cs.slots(nslots, 2 * (size_t)cs.n * 64 + 64);
@@ -453,6 +484,12 @@ int bpg_kernel_stats(const char *name, uint64_t *launches, double *total_ms, dou
     *launches = st.launches;
     *total_ms = st.total_ms;
     *alg_bytes = st.alg_bytes;
+    return 0;
+}
+int bpg_kernel_femul(const char *name, double *femul) {
+    KernelStat st;
+    if (!get_kernel_stat(name, st)) return -1;
+    *femul = st.femul;
     return 0;
 }
 void bpg_kernel_stats_reset(void) { reset_kernel_stats(); }

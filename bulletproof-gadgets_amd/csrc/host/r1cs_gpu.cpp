@@ -136,7 +136,7 @@ std::shared_ptr<CombTables> DeviceContext::ensure_comb(uint32_t N) {
 static std::atomic<bool> g_prof(false);
 static std::mutex g_prof_mu;
 static std::map<std::string, KernelStat> g_prof_stats;
-struct PendingEvent { const char *name; hipEvent_t a, b; double bytes; };
+struct PendingEvent { const char *name; hipEvent_t a, b; double bytes, femul; };
 int set_kernel_profiling(bool on) { g_prof = on; return 0; }
 bool get_kernel_stat(const char *name, KernelStat &out) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -148,7 +148,7 @@ bool get_kernel_stat(const char *name, KernelStat &out) {
 void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_stats.clear(); }
 
 // ---------------------------------------------------------------- workspace
-struct Workspace {
+struct Workspace : dev::ProfSink {
     int device = 0;
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
@@ -184,9 +184,9 @@ struct Workspace {
     }
     std::vector<PendingEvent> pend;
     // bracket the launches issued between begin() and end() on `st`
-    int prof_begin(const char *name, double bytes) {
+    int prof_begin(const char *name, double bytes, double femul = 0) {
         if (!g_prof) return -1;
-        PendingEvent e{name, nullptr, nullptr, bytes};
+        PendingEvent e{name, nullptr, nullptr, bytes, femul};
         BPG_HIP(hipEventCreate(&e.a));
         BPG_HIP(hipEventCreate(&e.b));
         BPG_HIP(hipEventRecord(e.a, st));
@@ -194,6 +194,8 @@ struct Workspace {
         return (int)pend.size() - 1;
     }
     void prof_end(int h) { if (h >= 0) BPG_HIP(hipEventRecord(pend[h].b, st)); }
+    int begin(const char *name, double bytes, double femul) override { return prof_begin(name, bytes, femul); }
+    void end(int h) override { prof_end(h); }
     void prof_flush() {   // call after the stream is synchronised
         if (pend.empty()) return;
         std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -204,6 +206,7 @@ struct Workspace {
                 k.launches++;
                 k.total_ms += ms;
                 k.alg_bytes += e.bytes;
+                k.femul += e.femul;
             }
             (void)hipEventDestroy(e.a);
             (void)hipEventDestroy(e.b);
@@ -231,6 +234,7 @@ Workspace &thread_workspace(int device) {
         BPG_HIP(hipHostMalloc((void **)&p->rows_host, 8 * 64 * sizeof(PtD), hipHostMallocDefault));
         BPG_HIP(hipHostMalloc((void **)&p->small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
     }
+    dev::set_prof_sink(p.get());   // this thread's launches record on its own stream
     BPG_HIP(hipSetDevice(device));
     return *p;
 }
@@ -798,17 +802,13 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                     radix16_digits(c3, C.dig[v][r][2]);
                 }
             }
-            int pf = ws.prof_begin("ipp_comb_fold", 2.0 * h1 * (4 * 64 + 64));
             launch_ipp_comb_fold(C, ws.comb_stage, st);
-            ws.prof_end(pf);
             Gh = ws.Gp[1].p; Hh = ws.Hp[1].p;
             gfmt = MSM_CACHED;
         } else if (h > 1) {
             PtD *Gn = as<PtD>(ws.Gp[k & 1]), *Hn = as<PtD>(ws.Hp[k & 1]);
-            int pf = ws.prof_begin("ipp_fold_points", 6.0 * h * 64);
             launch_ipp_fold_points(Gh, Hh, gfmt, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
                                    ws.fold_stage, st);
-            ws.prof_end(pf);
             Gh = Gn; Hh = Hn;
             gfmt = MSM_CACHED;
         }
@@ -851,6 +851,19 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
 // ------------------------------------------------------------------ verify
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V, const uint8_t *proof,
                size_t plen, const uint8_t entropy[32]) {
+    return gpu_verify_shard(cs, label, label_len, V, proof, plen, entropy, 0, 1, nullptr);
+}
+
+// One shard of Verifier::verify's mega-check. Every shard replays the
+// transcript and the rejection checks; shard s of S sums the generator terms
+// j in [s N/S, (s+1) N/S) of G and H, shard 0 also the proof/commitment
+// points and the B, B_blinding terms. The shards' partial sums add up to the
+// point that must be the identity; `partial` (32 B, compressed) receives this
+// shard's part. Returns 1 (partial written, or accept when S == 1), 0 reject.
+int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                     const uint8_t *proof, size_t plen, const uint8_t entropy[32], uint32_t shard, uint32_t nshards,
+                     uint8_t *partial) {
+    if (nshards < 1 || shard >= nshards) throw std::runtime_error("bad shard");
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t n = cs.n, m = cs.m, N = cs.N;
     // R1CSProof::from_bytes
@@ -992,18 +1005,24 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
     for (int i = 0; i < 5; i++) ss[3 + m + i] = to_dev(Ts[i]);
     for (uint32_t k = 0; k < lgn; k++) { ss[8 + m + k] = to_dev(u2[k]); ss[8 + m + lgn + k] = to_dev(ui2[k]); }
     BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
-    MsmSeg seg[3] = {{as<ScD>(ws.gh), ctx.G, N, 0}, {as<ScD>(ws.gh) + N, ctx.H, N, 0}, {sscal, ws.pts.p, ns, 0}};
-    MsmPlan pl = ws.msm->enqueue(seg, 3, 1, ws.rows_host, MSM_NIELS);
+    const uint64_t j0 = (uint64_t)N * shard / nshards, j1 = (uint64_t)N * (shard + 1) / nshards;
+    const uint32_t cnt = (uint32_t)(j1 - j0);
+    MsmSeg seg[3] = {{as<ScD>(ws.gh) + j0, ctx.G + j0, cnt, 0}, {as<ScD>(ws.gh) + N + j0, ctx.H + j0, cnt, 0},
+                     {sscal, ws.pts.p, ns, 0}};
+    MsmPlan pl = ws.msm->enqueue(seg, shard == 0 ? 3 : 2, 1, ws.rows_host, MSM_NIELS);
     ws.sync();
     Point R;
     combine_rows(R, ws.rows_host, pl.W, pl.c);
-    // B and B_blinding terms
-    Scalar sB = w * (tx - pa * pb) + r * (xx * (wc + delta) - tx);
-    Scalar sBb = -ebl - r * txb;
-    Point t1, t2;
-    mul_B(t1, sB); mul_B_blinding(t2, sBb);
-    pt_add(R, R, t1); pt_add(R, R, t2);
-    return pt_is_identity(R) ? 1 : 0;
+    if (shard == 0) {   // B and B_blinding terms
+        Scalar sB = w * (tx - pa * pb) + r * (xx * (wc + delta) - tx);
+        Scalar sBb = -ebl - r * txb;
+        Point t1, t2;
+        mul_B(t1, sB); mul_B_blinding(t2, sBb);
+        pt_add(R, R, t1); pt_add(R, R, t2);
+    }
+    if (nshards == 1) return pt_is_identity(R) ? 1 : 0;
+    ristretto_compress(partial, R);
+    return 1;
 }
 
 }  // namespace bpg

@@ -107,6 +107,11 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
 // Verifier::verify; returns 1 accept / 0 reject.
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                const uint8_t *proof, size_t proof_len, const uint8_t entropy[32]);
+// One shard of the verifier's mega-MSM (see r1cs_gpu.cpp); 1 = partial
+// written to `partial` (32 B), 0 = rejected by the shared checks.
+int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                     const uint8_t *proof, size_t proof_len, const uint8_t entropy[32], uint32_t shard,
+                     uint32_t nshards, uint8_t *partial);
 // Batched Pedersen commitments (V_i) on the device.
 void gpu_pedersen(int device, const std::vector<Scalar> &v, const std::vector<Scalar> &vb, uint8_t *out);
 // Generic MSM test hook.
@@ -116,7 +121,7 @@ ProveTimings &last_timings();
 
 // Live kernel instrumentation (bench.py roofline): HIP events around the hot
 // launches on their own stream, resolved after the stream synchronises.
-struct KernelStat { uint64_t launches = 0; double total_ms = 0, alg_bytes = 0; };
+struct KernelStat { uint64_t launches = 0; double total_ms = 0, alg_bytes = 0, femul = 0; };
 int set_kernel_profiling(bool on);
 bool get_kernel_stat(const char *name, KernelStat &out);
 void reset_kernel_stats();

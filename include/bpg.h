@@ -159,6 +159,25 @@ int bpg_r1cs_verify(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
                     const uint8_t *proof, size_t proof_len,
                     const uint8_t entropy[32]);
 
+/* Multi-GPU verification: shard `shard` of `nshards` of
+ * Verifier::verify's single mega-MSM. Every shard replays the transcript and
+ * the rejection checks; shard s sums the generator terms of its slice of G
+ * and H (shard 0 also the proof/commitment points and the B, B_blinding
+ * terms) and writes its partial sum, compressed, to `partial`. The proof is
+ * valid iff every shard returns 1 and the partials add up to the identity
+ * (bpg_point_sum -> 32 zero bytes). The exchange between GPUs is one
+ * all-gather of 32-byte partials (RCCL has no elliptic-curve reduction).
+ * Returns 1 partial written, 0 rejected, < 0 error. */
+int bpg_r1cs_verify_shard(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
+                          const bpg_r1cs_view *cs, const uint8_t *V,
+                          const uint8_t *proof, size_t proof_len,
+                          const uint8_t entropy[32], uint32_t shard,
+                          uint32_t nshards, uint8_t partial[32]);
+
+/* Host-only: out = sum of `count` compressed Ristretto points (identity =
+ * 32 zero bytes). Returns 0, or -1 if an input does not decompress. */
+int bpg_point_sum(const uint8_t *points, uint32_t count, uint8_t out[32]);
+
 /* Prepared (HBM-resident) circuit for repeated proving: uploads a_L/a_R/a_O
  * and the transposed constraint matrix once. */
 typedef struct bpg_prepared bpg_prepared;
@@ -213,6 +232,9 @@ int bpg_profile_enable(int on);
 int bpg_kernel_stats(const char *name, uint64_t *launches, double *total_ms,
                      double *alg_bytes);
 void bpg_kernel_stats_reset(void);
+/* Field multiplications (GF(2^255-19), squarings included) the recorded
+ * launches of `name` performed, for the VALU-side roofline. */
+int bpg_kernel_femul(const char *name, double *femul);
 
 /* Diagnostics for the batched RNG (lockstep STROBE / TranscriptRng for up
  * to 8 proofs, AVX-512 when available): self-test against the scalar

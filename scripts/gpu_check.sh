@@ -17,7 +17,9 @@ fi
 if [ "${PROF:-1}" = 1 ]; then
   ROOTD=$(pwd)
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $ROOTD/gpurun_out/${R}_prof -o run -- python3 $ROOTD/bench.py --steps 2 --threads ${PROF_THREADS:-2} --batch ${PROF_BATCH:-4} --no-cpu-baseline > $ROOTD/gpurun_out/${R}_prof_bench.json 2> $ROOTD/gpurun_out/${R}_prof.err
+  # the bench's own default command under the profiler (rocpd output; the
+  # CSV writer of rocprofv3 crashed with 16 host threads)
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $ROOTD/gpurun_out/${R}_prof -o run -- python3 $ROOTD/bench.py ${PROF_ARGS:-} > $ROOTD/gpurun_out/${R}_prof_bench.json 2> $ROOTD/gpurun_out/${R}_prof.err
   cd $ROOTD
 fi
 echo done

@@ -99,3 +99,31 @@ def test_config5_batch_equals_single(bpg, ctx, W):
     single, _ = ctx.r1cs_prove(b"b5", syn.view, ents[1])
     assert batch[1] == single
     assert len(set(batch)) == 3
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_sharded_verify(bpg, ctx, W, nshards):
+    """The verifier's mega-MSM split into shards (one per GPU under
+    torch.distributed; here all shards on one device): the partials of a
+    valid proof add up to the identity, a tampered proof's do not."""
+    inst, wit, gad = W.config2()
+    bpg.set_seed(7)
+    syn = bpg.Synth(inst, wit, gad)
+    proof, V = ctx.r1cs_prove(b"shard", syn.view, bytes([9]) * 32)
+
+    def verdict(pf):
+        msgs = []
+        for s in range(nshards):
+            ok, part = ctx.r1cs_verify_shard(b"shard", syn.view, V, pf, s, nshards)
+            msgs.append(bytes([1 if ok else 0]) + part)
+        if any(m[0] != 1 for m in msgs):
+            return False
+        return bpg.point_sum([m[1:] for m in msgs]) == b"\0" * 32
+
+    assert verdict(proof)
+    bad = bytearray(proof)
+    bad[417 + 5] ^= 1          # inside L_0
+    assert not verdict(bytes(bad))
+    bad = bytearray(proof)
+    bad[300] ^= 1              # t_x
+    assert not verdict(bytes(bad))
