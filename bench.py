@@ -26,6 +26,12 @@ import os
 import sys
 import time
 
+# HIP hardware queues per process (HIP's default is 4): each host consumer
+# thread drives its own stream, and with 4 queues streams share queues and
+# serialise behind each other's kernels (measured: profiles/r01h_sweep.txt).
+# Must be set before the HIP runtime initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -46,7 +52,7 @@ def parse():
 # single kernels bracketed live (bpg name -> rocprofv3 kernel name)
 KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1>", "msm_pass1_cached": "k_rbk_pass<true, 0>",
            "ipp_fold_points": "k_ipp_fold_points<gec>",
-           "ipp_comb_fold": "k_ipp_comb_fold", "flatten": "k_flatten_short"}
+           "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "flatten": "k_flatten_short"}
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 FEMUL_PEAK_G = 263.5         # GF(2^255-19) multiplies/s x1e9, measured (profiles/*_micro.log, fe_variants V2)
 

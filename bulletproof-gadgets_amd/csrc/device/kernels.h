@@ -171,6 +171,14 @@ struct CombArgs {
 };
 void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab, hipStream_t st);
 void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st);
+// Two-round Straus fold (no tables) from level-k generators (NielsD at level
+// 0, else PtD cached): out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1},
+// i < h1, the three scalar multiples sharing one doubling chain. coef[v][r][t]
+// (canonical, not Montgomery) is c_{t+1} of vector v (0 = G, 1 = H) for lanes
+// [rstart[r], rstart[r+1]).
+void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1, uint32_t nrange,
+                      const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][3], PtD *Gout, PtD *Hout,
+                      ArgStage &stage, hipStream_t st);
 // Round 1 of the lazy schedule: level-1 generators expanded into level 0.
 struct LazyArgs {
     uint32_t h0;              // round-0 half length (pairs j, j + h0)

@@ -1304,6 +1304,200 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
     BPG_HIP(hipGetLastError());
 }
 // ---------------------------------------------------------------------------
+// Two-round Straus fold (DESIGN.md "IPP fold in round pairs"). Lane i of the
+// output (level k+2) is P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1} over
+// the level-k points: one shared chain of ~252 doublings with the width-WN
+// NAF digits of the three scalars interleaved, instead of three single-scalar
+// folds (~3 x 252 doublings over 1.5x the lanes). The scalars are uniform per
+// lane range, so the merged op list (doublings before each addition, which
+// point, which odd multiple, sign) is built on the host and read with scalar
+// loads; blocks never straddle a range.
+// ---------------------------------------------------------------------------
+#ifndef BPG_FOLD2_WNAF
+#define BPG_FOLD2_WNAF 3
+#endif
+#define FOLD2_MAXSEG (2 * COMB_MAXRANGE)
+#define FOLD2_MAXOPS 400
+struct Fold2Args {
+    const void *in[2];
+    gec *out[2];
+    uint32_t h1, nseg;
+    uint32_t start[FOLD2_MAXSEG], end[FOLD2_MAXSEG], blk0[FOLD2_MAXSEG + 1], vec[FOLD2_MAXSEG];
+    uint32_t nops[FOLD2_MAXSEG], tail[FOLD2_MAXSEG];
+    // op: gap (doublings before it, 8 bits) | t << 8 (point 0..2) | (m >> 1) << 10 (odd multiple m) | neg << 15
+    uint16_t ops[FOLD2_MAXSEG][FOLD2_MAXOPS];
+};
+// LSB-first width-w NAF of a canonical scalar; returns the digit count
+static int wnaf_digits(const ScD &k, int w, int8_t d[264]) {
+    uint32_t x[9];
+    for (int i = 0; i < 8; i++) x[i] = k.v[i];
+    x[8] = 0;
+    const int full = 1 << w, half = full >> 1;
+    int len = 0;
+    auto nz = [&]() { for (int i = 0; i < 9; i++) if (x[i]) return true; return false; };
+    while (nz()) {
+        if (len >= 264) throw HipError(hipErrorInvalidValue, "wnaf length", __FILE__, __LINE__);
+        int di = 0;
+        if (x[0] & 1) {
+            di = (int)(x[0] & (uint32_t)(full - 1));
+            if (di >= half) di -= full;
+            if (di > 0) {
+                uint64_t bw = (uint64_t)di;
+                for (int i = 0; i < 9 && bw; i++) { uint64_t t = (uint64_t)x[i] - bw; x[i] = (uint32_t)t; bw = (t >> 63) & 1; }
+            } else {
+                uint64_t c = (uint64_t)(-di);
+                for (int i = 0; i < 9 && c; i++) { c += x[i]; x[i] = (uint32_t)c; c >>= 32; }
+            }
+        }
+        d[len++] = (int8_t)di;
+        for (int i = 0; i < 8; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+        x[8] >>= 1;
+    }
+    return len;
+}
+// selects the cached multiple m (1 or 3) of point t; uniform branches
+template <int WN>
+DEVI void fold2_pick(gec &r, const gec (&tp)[3][WN == 3 ? 2 : 1], uint32_t t, uint32_t mi) {
+    if constexpr (WN == 3) {
+        if (t == 0) r = mi ? tp[0][1] : tp[0][0];
+        else if (t == 1) r = mi ? tp[1][1] : tp[1][0];
+        else r = mi ? tp[2][1] : tp[2][0];
+    } else {
+        (void)mi;
+        if (t == 0) r = tp[0][0]; else if (t == 1) r = tp[1][0]; else r = tp[2][0];
+    }
+}
+// WN = 3: odd multiples P, 3P of the three points in registers (one wave per
+// SIMD); WN = 2: P only (NAF, two waves per SIMD)
+template <class P, int WN>
+__global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Args *__restrict__ Ap) {
+    const Fold2Args &A = *Ap;
+    uint32_t b = blockIdx.x, sg = 0;
+    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
+    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
+    if (i >= A.end[sg]) return;
+    const uint32_t v = A.vec[sg], nops = A.nops[sg];
+    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
+    const uint16_t *ops = A.ops[sg];
+    const uint32_t h1 = A.h1;
+    gec P0;
+    if (nops == 0) {
+        load_as_cached(P0, Pin + i);
+        gec_store(A.out[v] + i, P0);
+        return;
+    }
+    gec tp[3][WN == 3 ? 2 : 1];
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        load_as_cached(tp[t][0], Pin + (size_t)(t + 1) * h1 + i);
+        if constexpr (WN == 3) {
+        ge pr, p2, q;
+        fe_sub(pr.X, tp[t][0].YpX, tp[t][0].YmX);   // projective (2X : 2Y : 2Z), enough to double
+        fe_add(pr.Y, tp[t][0].YpX, tp[t][0].YmX);
+        pr.Z = tp[t][0].Z2;
+        ge_dbl(p2, pr);
+        ge_add_c(q, p2, tp[t][0]);
+        ge_to_cached(tp[t][1], q);
+        }
+    }
+    ge acc;
+    {
+        const uint32_t op = ops[0];
+        gec c;
+        fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31);
+        if (op >> 15) gec_neg(c, c);
+        ge_from_cached(acc, c);
+    }
+    for (uint32_t k = 1; k < nops; k++) {
+        const uint32_t op = ops[k];
+        const uint32_t g = op & 255;
+        if (g) {
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        gec c;
+        fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31);
+        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+    }
+    const uint32_t tail = A.tail[sg];
+    if (tail) {
+        for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
+        ge_dbl_t<true>(acc, acc);
+    }
+    load_as_cached(P0, Pin + i);
+    ge r;
+    ge_add_c(r, acc, P0);
+    gec out;
+    ge_to_cached(out, r);
+    gec_store(A.out[v] + i, out);
+}
+void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1, uint32_t nrange,
+                      const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][3], PtD *Gout, PtD *Hout,
+                      ArgStage &stage, hipStream_t st) {
+    if (!h1) return;
+    if (nrange < 1 || nrange > COMB_MAXRANGE) throw HipError(hipErrorInvalidValue, "fold2 ranges", __FILE__, __LINE__);
+    if (!stage.dev) {
+        BPG_HIP(hipMalloc(&stage.dev, sizeof(Fold2Args)));
+        BPG_HIP(hipHostMalloc(&stage.host, sizeof(Fold2Args), hipHostMallocDefault));
+        BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
+    } else {
+        BPG_HIP(hipEventSynchronize(stage.copied));   // previous upload has left the host buffer
+    }
+    Fold2Args &A = *reinterpret_cast<Fold2Args *>(stage.host);
+    A.in[0] = Gin; A.in[1] = Hin;
+    A.out[0] = AS_GEC(Gout); A.out[1] = AS_GEC(Hout);
+    A.h1 = h1;
+    A.nseg = 0;
+    uint32_t blocks = 0;
+    double fem = 0;
+    static const int WN = [] { const char *e = getenv("BPG_FOLD2_W"); return (e && atoi(e) == 2) ? 2 : BPG_FOLD2_WNAF; }();
+    for (uint32_t v = 0; v < 2; v++)
+        for (uint32_t r = 0; r < nrange; r++) {
+            const uint32_t lo = rstart[r], hi = r + 1 < nrange ? rstart[r + 1] : h1;
+            if (hi <= lo) continue;
+            const uint32_t s = A.nseg++;
+            A.start[s] = lo; A.end[s] = hi; A.vec[s] = v; A.blk0[s] = blocks;
+            blocks += nblk(hi - lo, 64);
+            int8_t d[3][264];
+            int len[3], top = -1;
+            for (int t = 0; t < 3; t++) {
+                len[t] = wnaf_digits(coef[v][r][t], WN, d[t]);
+                top = std::max(top, len[t] - 1);
+            }
+            uint32_t n = 0, dbl = 0;
+            int last = -1;
+            for (int pos = top; pos >= 0; pos--)
+                for (int t = 0; t < 3; t++) {
+                    if (pos >= len[t] || !d[t][pos]) continue;
+                    if (n >= FOLD2_MAXOPS) throw HipError(hipErrorInvalidValue, "fold2 ops", __FILE__, __LINE__);
+                    const int dg = d[t][pos], m = dg < 0 ? -dg : dg;
+                    const uint32_t gap = last < 0 ? 0u : (uint32_t)(last - pos);
+                    if (gap > 255) throw HipError(hipErrorInvalidValue, "fold2 gap", __FILE__, __LINE__);
+                    A.ops[s][n++] = (uint16_t)(gap | ((uint32_t)t << 8) | ((uint32_t)(m >> 1) << 10) |
+                                               ((dg < 0 ? 1u : 0u) << 15));
+                    dbl += gap;
+                    last = pos;
+                }
+            A.nops[s] = n;
+            A.tail[s] = last < 0 ? 0u : (uint32_t)last;
+            dbl += A.tail[s];
+            fem += (double)(hi - lo) * (7.0 * dbl + 8.0 * n + (WN == 3 ? 3 * 17.0 : 0.0) + 12.0);
+        }
+    A.blk0[A.nseg] = blocks;
+    if (!blocks) return;
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(Fold2Args), hipMemcpyHostToDevice, st));
+    BPG_HIP(hipEventRecord(stage.copied, st));
+    // reads 4 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
+    ProfScope ps("ipp_fold2", 2.0 * h1 * 5 * 64, fem);
+    const Fold2Args *dA = reinterpret_cast<const Fold2Args *>(stage.dev);
+    if (in_fmt == MSM_NIELS && WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gen, 3>), dim3(blocks), dim3(64), 0, st, dA);
+    else if (in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2<gen, 2>), dim3(blocks), dim3(64), 0, st, dA);
+    else if (WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gec, 3>), dim3(blocks), dim3(64), 0, st, dA);
+    else hipLaunchKernelGGL((k_ipp_fold2<gec, 2>), dim3(blocks), dim3(64), 0, st, dA);
+    BPG_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
 // Comb tables and the two-round table fold (DESIGN.md "IPP rounds 0-1").
 // For generator j = j0 + jj (jj < ntab): entry (w, d) = (d+1) 16^w P_j for
 // w < 64, d < 8, packed affine Niels (96 B) at 16-byte unit

@@ -72,6 +72,11 @@ int bpg_set_fold_tables(int mode) {
     set_fold_tables(mode);
     return 0;
 }
+int bpg_set_fold_pairs(int mode) {
+    if (mode < -1 || mode > 1) return -1;
+    set_fold_pairs(mode);
+    return 0;
+}
 int bpg_set_device(int device) {
     if (device < 0) return -1;
     g_device = device;

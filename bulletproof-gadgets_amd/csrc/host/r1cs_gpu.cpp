@@ -99,6 +99,14 @@ static bool fold_tables_enabled() {
     const char *e = getenv("BPG_FOLD_TABLES");
     return !(e && e[0] == '0');
 }
+static std::atomic<int> g_fold_pairs(-1);
+void set_fold_pairs(int mode) { g_fold_pairs = mode; }
+static bool fold_pairs_enabled() {
+    int m = g_fold_pairs;
+    if (m >= 0) return m != 0;
+    const char *e = getenv("BPG_FOLD_PAIRS");
+    return !(e && e[0] == '0');
+}
 CombTables::~CombTables() {
     if (tabG || tabH) (void)hipSetDevice(device);
     if (tabG) (void)hipFree(tabG);
@@ -160,6 +168,7 @@ struct Workspace : dev::ProfSink {
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
     dev::ArgStage fold_stage;        // IPP fold kernel arguments
     dev::ArgStage comb_stage;        // table-fold kernel arguments
+    dev::ArgStage fold2_stage;       // two-round Straus fold kernel arguments
     hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
     void sync() {
         BPG_HIP(hipEventRecord(done_ev, st));
@@ -173,6 +182,9 @@ struct Workspace : dev::ProfSink {
         if (comb_stage.dev) (void)hipFree(comb_stage.dev);
         if (comb_stage.host) (void)hipHostFree(comb_stage.host);
         if (comb_stage.copied) (void)hipEventDestroy(comb_stage.copied);
+        if (fold2_stage.dev) (void)hipFree(fold2_stage.dev);
+        if (fold2_stage.host) (void)hipHostFree(fold2_stage.host);
+        if (fold2_stage.copied) (void)hipEventDestroy(fold2_stage.copied);
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
@@ -716,7 +728,14 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     if (N >= 2) {
         for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(N / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(N / 2) * sizeof(PtD)); }
     }
-    Scalar rho0[4];   // round-0 fold scalars (G a/b, H a/b) for the table pass
+    // Round pairs: after round k the fold is left pending (Ghat stays at level
+    // k); round k+1's MSM expands each level-(k+1) base into its two level-k
+    // points, and level k+2 is built from level k in one pass (comb tables from
+    // the level-0 generators, else the three-scalar Straus fold).
+    const bool pairs = fold_pairs_enabled();
+    Scalar rho_p[4];   // pending fold's scalars (G a/b, H a/b)
+    bool pend = false;
+    int cur = -1;      // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
     uint32_t len = N;
     for (uint32_t k = 0; len != 1; k++) {
         const uint32_t h = len / 2;
@@ -726,27 +745,26 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         A.muH1 = mont(mu); A.muHu = mont(mu * u);
         ScD *ms = as<ScD>(ws.mscal);
         const void *Qb = gfmt == MSM_NIELS ? (const void *)Qn : (const void *)Qc;
+        const size_t ps = gfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
+        auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
         MsmSeg seg[10];
         int nseg;
-        const bool lazy = comb && k == 1;
+        const bool lazy = pend;
         if (lazy) {
             const uint32_t h0 = 2 * h;
             LazyArgs Z;
             Z.h0 = h0;
-            Z.rGa = mont(rho0[0]); Z.rGb = mont(rho0[1]); Z.rHa = mont(rho0[2]); Z.rHb = mont(rho0[3]);
+            Z.rGa = mont(rho_p[0]); Z.rGb = mont(rho_p[1]); Z.rHa = mont(rho_p[2]); Z.rHb = mont(rho_p[3]);
             launch_ipp_prep_lazy(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
-            const NielsD *G0 = ctx.G, *H0 = ctx.H;
             const size_t hh = h;
-            MsmSeg sl[10] = {{ms, G0 + h, h, 0}, {ms + hh, G0 + h + h0, h, 0}, {ms + 2 * hh, H0, h, 0},
-                             {ms + 3 * hh, H0 + h0, h, 0}, {ms + 8 * hh, Qb, 1, 0},
-                             {ms + 4 * hh, G0, h, 1}, {ms + 5 * hh, G0 + h0, h, 1}, {ms + 6 * hh, H0 + h, h, 1},
-                             {ms + 7 * hh, H0 + h + h0, h, 1}, {ms + 8 * hh + 1, Qb, 1, 1}};
+            MsmSeg sl[10] = {{ms, at(Gh, h), h, 0}, {ms + hh, at(Gh, h + h0), h, 0}, {ms + 2 * hh, Hh, h, 0},
+                             {ms + 3 * hh, at(Hh, h0), h, 0}, {ms + 8 * hh, Qb, 1, 0},
+                             {ms + 4 * hh, Gh, h, 1}, {ms + 5 * hh, at(Gh, h0), h, 1}, {ms + 6 * hh, at(Hh, h), h, 1},
+                             {ms + 7 * hh, at(Hh, h + h0), h, 1}, {ms + 8 * hh + 1, Qb, 1, 1}};
             std::copy(sl, sl + 10, seg);
             nseg = 10;
         } else {
             launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-            const size_t ps = gfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
-            auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
             const size_t hh = h;
             MsmSeg sl[6] = {{ms, at(Gh, h), h, 0}, {ms + hh, Hh, h, 0}, {ms + 4 * hh, Qb, 1, 0},
                             {ms + 2 * hh, Gh, h, 1}, {ms + 3 * hh, at(Hh, h), h, 1}, {ms + 4 * hh + 1, Qb, 1, 1}};
@@ -771,46 +789,66 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         Scalar u2 = uk * uk, ui2 = uinv * uinv;
         Scalar yh = sc_pow_u64(y_inv, h);
         Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
-        if (comb && k == 0) {
-            rho0[0] = rGa; rho0[1] = rGb; rho0[2] = rHa; rho0[3] = rHb;   // level 1 stays implicit
-        } else if (lazy && h > 1) {
-            // level 2 from level 0: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
-            const uint32_t h1 = h, h0 = 2 * h;
-            CombArgs C{};
-            C.gens[0] = ctx.G; C.gens[1] = ctx.H;
-            C.tab[0] = comb->tabG; C.tab[1] = comb->tabH;
-            C.out[0] = ws.Gp[1].p; C.out[1] = ws.Hp[1].p;
-            C.h1 = h1; C.ntab = 3 * h1;
-            std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)n - h1, (int64_t)n, (int64_t)n - h0,
-                                        (int64_t)n - h0 - h1};
-            std::vector<uint32_t> starts;
-            for (int64_t c : cut) if (c >= 0 && c < (int64_t)h1) starts.push_back((uint32_t)c);
-            std::sort(starts.begin(), starts.end());
-            starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
-            C.nrange = (uint32_t)starts.size();
-            const Scalar r1[4] = {rGa, rGb, rHa, rHb};
-            for (uint32_t r = 0; r < C.nrange; r++) {
-                const uint64_t i = starts[r];
-                C.rstart[r] = (uint32_t)i;
-                const bool b1 = i < n && i + h1 >= n, b0 = i < n && i + h0 >= n, b0h = i + h1 < n && i + h1 + h0 >= n;
-                for (int v = 0; v < 2; v++) {
-                    const Scalar c1 = r1[2 * v + (b1 ? 1 : 0)];
-                    const Scalar c2 = rho0[2 * v + (b0 ? 1 : 0)];
-                    const Scalar c3 = c1 * rho0[2 * v + (b0h ? 1 : 0)];
-                    radix16_digits(c1, C.dig[v][r][0]);
-                    radix16_digits(c2, C.dig[v][r][1]);
-                    radix16_digits(c3, C.dig[v][r][2]);
+        const int nxt = cur == 0 ? 1 : 0;
+        if (lazy) {
+            pend = false;
+            if (h > 1) {
+                // level k+1 from level k-1: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
+                const uint32_t h1 = h, h0 = 2 * h;
+                std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)n - h1, (int64_t)n, (int64_t)n - h0,
+                                            (int64_t)n - h0 - h1};
+                std::vector<uint32_t> starts;
+                for (int64_t c : cut) if (c >= 0 && c < (int64_t)h1) starts.push_back((uint32_t)c);
+                std::sort(starts.begin(), starts.end());
+                starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+                const Scalar r1[4] = {rGa, rGb, rHa, rHb};
+                ScD coef[2][COMB_MAXRANGE][3];
+                const bool table = comb && cur < 0;
+                CombArgs C{};
+                C.nrange = (uint32_t)starts.size();
+                for (uint32_t r = 0; r < C.nrange; r++) {
+                    const uint64_t i = starts[r];
+                    C.rstart[r] = (uint32_t)i;
+                    const bool b1 = i < n && i + h1 >= n, b0 = i < n && i + h0 >= n, b0h = i + h1 < n && i + h1 + h0 >= n;
+                    for (int v = 0; v < 2; v++) {
+                        const Scalar c1 = r1[2 * v + (b1 ? 1 : 0)];
+                        const Scalar c2 = rho_p[2 * v + (b0 ? 1 : 0)];
+                        const Scalar c3 = c1 * rho_p[2 * v + (b0h ? 1 : 0)];
+                        if (table) {
+                            radix16_digits(c1, C.dig[v][r][0]);
+                            radix16_digits(c2, C.dig[v][r][1]);
+                            radix16_digits(c3, C.dig[v][r][2]);
+                        } else {
+                            coef[v][r][0] = to_dev(c1); coef[v][r][1] = to_dev(c2); coef[v][r][2] = to_dev(c3);
+                        }
+                    }
                 }
+                if (table) {
+                    C.gens[0] = ctx.G; C.gens[1] = ctx.H;
+                    C.tab[0] = comb->tabG; C.tab[1] = comb->tabH;
+                    C.out[0] = ws.Gp[nxt].p; C.out[1] = ws.Hp[nxt].p;
+                    C.h1 = h1; C.ntab = 3 * h1;
+                    launch_ipp_comb_fold(C, ws.comb_stage, st);
+                } else {
+                    launch_ipp_fold2(Gh, Hh, gfmt, h1, C.nrange, C.rstart, coef, as<PtD>(ws.Gp[nxt]),
+                                     as<PtD>(ws.Hp[nxt]), ws.fold2_stage, st);
+                }
+                Gh = ws.Gp[nxt].p; Hh = ws.Hp[nxt].p;
+                cur = nxt;
+                gfmt = MSM_CACHED;
             }
-            launch_ipp_comb_fold(C, ws.comb_stage, st);
-            Gh = ws.Gp[1].p; Hh = ws.Hp[1].p;
-            gfmt = MSM_CACHED;
         } else if (h > 1) {
-            PtD *Gn = as<PtD>(ws.Gp[k & 1]), *Hn = as<PtD>(ws.Hp[k & 1]);
-            launch_ipp_fold_points(Gh, Hh, gfmt, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
-                                   ws.fold_stage, st);
-            Gh = Gn; Hh = Hn;
-            gfmt = MSM_CACHED;
+            if (pairs || (comb && cur < 0)) {
+                rho_p[0] = rGa; rho_p[1] = rGb; rho_p[2] = rHa; rho_p[3] = rHb;   // level k+1 stays implicit
+                pend = true;
+            } else {
+                PtD *Gn = as<PtD>(ws.Gp[nxt]), *Hn = as<PtD>(ws.Hp[nxt]);
+                launch_ipp_fold_points(Gh, Hh, gfmt, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
+                                       ws.fold_stage, st);
+                Gh = Gn; Hh = Hn;
+                cur = nxt;
+                gfmt = MSM_CACHED;
+            }
         }
         lam = lam * uinv;
         mu = mu * uk;

@@ -49,6 +49,8 @@ struct DeviceContext {
 };
 // -1 auto (env BPG_FOLD_TABLES, default on), 0 off, 1 on
 void set_fold_tables(int mode);
+// -1 auto (env BPG_FOLD_PAIRS, default on), 0 off, 1 on
+void set_fold_pairs(int mode);
 
 // Flattened circuit resident on the device (inputs in HBM before timing).
 struct PreparedCS {

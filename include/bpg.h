@@ -87,6 +87,13 @@ int bpg_set_device(int device);
  * identical either way. */
 int bpg_set_fold_tables(int mode);
 
+/* Added: IPP point folds in round pairs (process-wide). mode 1: rounds k, k+1
+ * fold together (level k+2 from level k by a three-scalar Straus pass, round
+ * k+1's MSM over the level-k points); mode 0: one fold per round; -1:
+ * automatic (pairs; env BPG_FOLD_PAIRS=0 disables). Proof bytes are identical
+ * either way. */
+int bpg_set_fold_pairs(int mode);
+
 /* ------------------------------------------------------------------------ */
 /* 2. Inner operator ABI: the flattened constraint system                     */
 /* ------------------------------------------------------------------------ */

@@ -68,14 +68,18 @@ def test_full_size_verify_and_strategies(bpg, ctx, W, cfg):
     ent = bytes([cfg]) * 32
     lib = bpg.lib()
     proofs = []
-    for mode in (1, 0):
-        assert lib.bpg_set_fold_tables(mode) == 0
+    # (comb tables, round-pair folds): table pass + Straus pair folds, Straus
+    # pair folds only, one variable-base fold per round
+    for tables, pairs in ((1, 1), (0, 1), (0, 0)):
+        assert lib.bpg_set_fold_tables(tables) == 0
+        assert lib.bpg_set_fold_pairs(pairs) == 0
         try:
             p, V = ctx.r1cs_prove(b"scale", syn.view, ent)
         finally:
             lib.bpg_set_fold_tables(-1)
+            lib.bpg_set_fold_pairs(-1)
         proofs.append(p)
-    assert proofs[0] == proofs[1]
+    assert proofs[0] == proofs[1] == proofs[2]
     proof = proofs[0]
     N = 1
     while N < syn.n:
