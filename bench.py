@@ -50,7 +50,7 @@ def parse():
 
 
 # single kernels bracketed live (bpg name -> rocprofv3 kernel name)
-KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1>", "msm_pass1_cached": "k_rbk_pass<true, 0>",
+KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1>", "msm_pass1_affine": "k_rbk_pass<true, 2>", "msm_pass1_cached": "k_rbk_pass<true, 0>",
            "ipp_fold_points": "k_ipp_fold_points<gec>",
            "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "flatten": "k_flatten_short"}
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)

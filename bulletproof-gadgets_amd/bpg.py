@@ -26,7 +26,7 @@ EXPORTS = [
     "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free", "bpg_mimc_hash",
     "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
     "bpg_rng_rate", "bpg_set_fold_tables", "bpg_r1cs_verify_shard", "bpg_point_sum",
-    "bpg_kernel_femul", "bpg_set_fold_pairs",
+    "bpg_kernel_femul", "bpg_set_fold_pairs", "bpg_set_msm_affine", "bpg_set_msm_fixed",
 ]
 
 
@@ -78,6 +78,8 @@ def lib():
         L.bpg_point_sum.argtypes = [vp, u32, vp]
         L.bpg_set_fold_tables.argtypes = [ctypes.c_int]
         L.bpg_set_fold_pairs.argtypes = [ctypes.c_int]
+        L.bpg_set_msm_affine.argtypes = [ctypes.c_int]
+        L.bpg_set_msm_fixed.argtypes = [ctypes.c_int]
         L.bpg_prepare.restype = vp
         L.bpg_prepare.argtypes = [vp, vp]
         L.bpg_prepared_free.argtypes = [vp]

@@ -68,9 +68,21 @@ struct MsmSeg {
     const void *base;  // PtD (cached) or NielsD, per the job's format
     uint32_t count;
     uint32_t msm;      // which MSM of the job this segment contributes to
+    // Fixed-base window table: nonzero = window w of point i lives at
+    // base[i + w * wstride] as 2^(WTAB_C w) P_i (all segments of a job or none)
+    uint32_t wstride = 0;
 };
+// Fixed-base window tables of the generators (DESIGN.md "Fixed-base MSMs"):
+// entry [w * N + j] = 2^(16 w) P_j, affine Niels, w < WTAB_W. A job over
+// tables puts all windows of an MSM into one row of 2^15 buckets: no
+// per-window bucket reduction, no host doublings, 16-bit sort keys.
+#define WTAB_C 16
+#define WTAB_W 16
+void launch_wtab_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st);
 struct MsmPlan {
-    int c, W, nmsm, rows, half;
+    int c, W, nmsm, rows, half;   // W: rows per MSM (1 for fixed-base jobs)
+    int Wd;                       // digit windows per scalar
+    bool fixed;
     uint64_t total;         // points in the job
     uint64_t E0;            // W * total
     uint32_t T;             // chunk size of the reduce-by-key passes

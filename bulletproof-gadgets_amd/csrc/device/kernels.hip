@@ -233,8 +233,10 @@ struct SegTab {
     const void *base[MSM_MAXSEG];
     uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t row0[MSM_MAXSEG];
+    uint32_t wstride[MSM_MAXSEG];   // fixed-base jobs: points between window tables
     int n;
 };
+#define MSM_VAL_G 0x00ffffffu       // val = sign << 31 | window << 24 (fixed-base) | point
 DEVI int seg_of(const SegTab &T, uint32_t g) {
     int si = 0;
 #pragma unroll
@@ -242,8 +244,10 @@ DEVI int seg_of(const SegTab &T, uint32_t g) {
     return si;
 }
 
-// signed c-bit windows; key = row * half + (|d| - 1), val = point | sign << 31
-__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t half, uint32_t invalid,
+// signed c-bit windows; key = (row + w * wrow) * half + (|d| - 1), val = point | sign << 31
+// (wrow = 1: one row per window; wrow = 0, fixed-base: one row per MSM and the
+// window goes into the value)
+__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t wrow, uint32_t half, uint32_t invalid,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
@@ -259,14 +263,15 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t ha
         if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
         uint32_t d = (uint32_t)(x >> sh) & mask;
         d += carry;
-        uint32_t key = invalid, val = g;
+        const uint32_t rw = row + (uint32_t)w * wrow;
+        uint32_t key = invalid, val = g | (wrow ? 0u : (uint32_t)w << 24);
         if (d > half) {
             uint32_t mag = full - d;
             carry = 1;
-            if (mag) { key = (row + w) * half + (mag - 1); val = g | 0x80000000u; }
+            if (mag) { key = rw * half + (mag - 1); val |= 0x80000000u; }
         } else {
             carry = 0;
-            if (d) key = (row + w) * half + (d - 1);
+            if (d) key = rw * half + (d - 1);
         }
         keys[(size_t)w * total + g] = key;
         vals[(size_t)w * total + g] = val;
@@ -281,13 +286,15 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t ha
 // Stable ranking inside a wave: 7 ballots give each lane the mask of lanes
 // holding its digit; rank = popcount of that mask below the lane.
 // ---------------------------------------------------------------------------
-#define RS_BITS 7
-#define RS_BINS 128
+// Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
+#define RS_MAXBINS 256
 #define RS_BLOCK 256
 #define RS_ROUNDS 8
 #define RS_ITER (RS_BLOCK * RS_ROUNDS)
+template <int RS_BITS>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict__ keys, uint32_t E, int shift,
                                                       uint32_t tile, uint32_t nb, uint32_t *__restrict__ hist) {
+    constexpr uint32_t RS_BINS = 1u << RS_BITS;
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
@@ -325,11 +332,13 @@ __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist,
 // rank keys within their digit, the iteration is reordered by digit in LDS,
 // then written out so that lanes with consecutive LDS slots of one digit
 // write consecutive addresses.
+template <int RS_BITS>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                          uint32_t E, int shift, uint32_t tile, uint32_t nb,
                                                          const uint32_t *__restrict__ hist,
                                                          const uint32_t *__restrict__ total,
                                                          uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+    constexpr uint32_t RS_BINS = 1u << RS_BITS;
     __shared__ uint32_t base[RS_BINS], lstart[RS_BINS], tot[RS_BINS];
     __shared__ uint32_t cnt[RS_ROUNDS][RS_BLOCK / 64][RS_BINS];
     __shared__ uint32_t lk[RS_ITER], lv[RS_ITER];
@@ -435,9 +444,10 @@ template <> struct BaseOf<MSM_NIELS> { typedef gen T; };
 template <> struct BaseOf<MSM_AFFINE> { typedef gaf T; };
 template <int FMT>
 DEVI void msm_load_base(typename BaseOf<FMT>::T &p, const SegTab &T, uint32_t v) {
-    const uint32_t g = v & 0x7fffffffu;
+    const uint32_t g = v & MSM_VAL_G, w = (v >> 24) & 0x7fu;
     const int si = seg_of(T, g);
-    pt_load(p, reinterpret_cast<const typename BaseOf<FMT>::T *>(T.base[si]) + (g - T.gofs[si]));
+    pt_load(p, reinterpret_cast<const typename BaseOf<FMT>::T *>(T.base[si]) + (g - T.gofs[si]) +
+                   (size_t)w * T.wstride[si]);
 }
 DEVI void msm_add_loaded(ge &acc, gen &p, bool neg) { gen_cneg(p, neg); ge_madd(acc, acc, p); }
 DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) { gec_cneg(p, neg); ge_add_c(acc, acc, p); }
@@ -688,13 +698,13 @@ void DBuf::grow(size_t need) {
 void MsmEngine::reserve(const MsmPlan &p) {
     size_t kb = p.E0 * 4;
     keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
-    sort_tmp_.grow((size_t)RS_BINS * 2049 * 4 + 256);       // radix-sort block histograms + totals
+    sort_tmp_.grow((size_t)RS_MAXBINS * 2049 * 4 + 256);    // radix-sort block histograms + totals
     rk_a_.grow(p.capE * 4); rp_a_.grow(p.capE * sizeof(ge));
     rk_b_.grow(p.capE * 4 / 4 + 1024); rp_b_.grow((p.capE / 4 + 256) * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
     bflag_.grow((size_t)p.rows * p.half);
     segacc_.grow((size_t)2 * p.rows * p.nseg_per_row * sizeof(ge));
-    rows_dev_.grow((size_t)p.rows * sizeof(ge));
+    rows_dev_.grow((size_t)p.rows * 257 * sizeof(ge));   // rows + per-block parts (split <= 256)
 }
 
 // sort (keys, vals) -> sorted pairs; returns which buffers hold them
@@ -704,12 +714,23 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
     const uint32_t nb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (E + 4095) / 4096));
     uint64_t tile = (E + nb - 1) / nb;
     tile = (tile + RS_ITER - 1) / RS_ITER * RS_ITER;
-    uint32_t *total = hist + (size_t)RS_BINS * nb;
-    for (int shift = 0; shift < key_bits; shift += RS_BITS) {
-        hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_BLOCK), 0, st, k, (uint32_t)E, shift, (uint32_t)tile, nb, hist);
-        hipLaunchKernelGGL(k_rs_colscan, dim3(RS_BINS), dim3(256), 0, st, hist, nb, total);
-        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_BLOCK), 0, st, k, v, (uint32_t)E, shift, (uint32_t)tile, nb,
-                           hist, total, k2, v2);
+    // 8-bit digits only where they save a pass (their scatter costs more LDS)
+    static const bool sort8 = [] { const char *e = getenv("BPG_SORT8"); return !(e && e[0] == '0'); }();
+    const int bits = sort8 && (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
+    const uint32_t bins = 1u << bits;
+    uint32_t *total = hist + (size_t)bins * nb;
+    for (int shift = 0; shift < key_bits; shift += bits) {
+        if (bits == 8)
+            hipLaunchKernelGGL(k_rs_hist<8>, dim3(nb), dim3(RS_BLOCK), 0, st, k, (uint32_t)E, shift, (uint32_t)tile, nb, hist);
+        else
+            hipLaunchKernelGGL(k_rs_hist<7>, dim3(nb), dim3(RS_BLOCK), 0, st, k, (uint32_t)E, shift, (uint32_t)tile, nb, hist);
+        hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nb, total);
+        if (bits == 8)
+            hipLaunchKernelGGL(k_rs_scatter<8>, dim3(nb), dim3(RS_BLOCK), 0, st, k, v, (uint32_t)E, shift, (uint32_t)tile,
+                               nb, hist, total, k2, v2);
+        else
+            hipLaunchKernelGGL(k_rs_scatter<7>, dim3(nb), dim3(RS_BLOCK), 0, st, k, v, (uint32_t)E, shift, (uint32_t)tile,
+                               nb, hist, total, k2, v2);
         std::swap(k, k2);
         std::swap(v, v2);
     }
@@ -724,11 +745,21 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     SegTab T{};
     uint64_t total = 0;
     T.n = nseg;
-    for (int i = 0; i < nseg; i++) { T.gofs[i] = (uint32_t)total; total += segs[i].count; }
+    int nfixed = 0;
+    for (int i = 0; i < nseg; i++) {
+        T.gofs[i] = (uint32_t)total;
+        total += segs[i].count;
+        nfixed += segs[i].wstride ? 1 : 0;
+    }
+    if (nfixed && nfixed != nseg) throw HipError(hipErrorInvalidValue, "mixed fixed-base job", __FILE__, __LINE__);
+    if (total > MSM_VAL_G) throw HipError(hipErrorInvalidValue, "msm job too large", __FILE__, __LINE__);
     T.gofs[nseg] = (uint32_t)total;
     p.total = total;
-    p.c = msm_window(total);
-    p.W = (254 + p.c - 1) / p.c;
+    p.fixed = nfixed > 0;
+    p.c = p.fixed ? WTAB_C : msm_window(total);
+    p.Wd = (254 + p.c - 1) / p.c;
+    if (p.fixed && p.Wd != WTAB_W) throw HipError(hipErrorInvalidValue, "window table", __FILE__, __LINE__);
+    p.W = p.fixed ? 1 : p.Wd;
     p.nmsm = nmsm;
     p.rows = nmsm * p.W;
     p.half = 1 << (p.c - 1);
@@ -736,8 +767,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         T.scal[i] = AS_CSC(segs[i].scal);
         T.base[i] = segs[i].base;
         T.row0[i] = segs[i].msm * p.W;
+        T.wstride[i] = segs[i].wstride;
     }
-    p.E0 = (uint64_t)p.W * total;
+    p.E0 = (uint64_t)p.Wd * total;
     p.T = RBK_T;
     uint64_t D = (uint64_t)p.rows * p.half;
     uint32_t invalid = (uint32_t)D;
@@ -759,8 +791,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     uint8_t *bflag = (uint8_t *)bflag_.p;
     ge *buckets = AS_GE(buckets_.p);
     BPG_HIP(hipMemsetAsync(bflag, 0, D, st_));
-    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
-                       (uint32_t)p.half, invalid, keys, vals);
+    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.Wd,
+                       p.fixed ? 0u : 1u, (uint32_t)p.half, invalid, keys, vals);
     BPG_HIP(hipGetLastError());
     radix_sort(keys, vals, keys2, vals2, p.E0, (int)p.key_bits, (uint32_t *)sort_tmp_.p, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
@@ -773,8 +805,11 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     for (;;) {
         const uint32_t nblocks = (uint32_t)std::max<uint64_t>(1, (E + RBK_CHUNK - 1) / RBK_CHUNK);
         // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
-        ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"), 96.0 * (double)total,
-                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);   // one mixed addition per entry
+        ProfScope ps(p.passes ? nullptr
+                              : (fmt == MSM_CACHED ? "msm_pass1_cached"
+                                                   : fmt == MSM_AFFINE ? "msm_pass1_affine" : "msm_pass1_niels"),
+                     96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels, 9M affine (2M to Niels)
+                     (fmt == MSM_CACHED ? 8.0 : fmt == MSM_AFFINE ? 9.0 : 7.0) * (double)p.E0);
         if (p.passes == 0 && fmt == MSM_NIELS)
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin, T,
                                E, invalid, kout, pout, buckets, bflag);
@@ -804,8 +839,24 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
                        (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, segA, segT);
     int lgL = 0;
     while ((1 << lgL) < p.seglen) lgL++;
-    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                       (uint32_t)p.nseg_per_row, lgL, 1u, AS_GE(rows_dev_.p));
+    // split rows over several blocks so the level-2 reduction is not a
+    // handful of long serial chains (latency-bound at rows x 256 threads)
+    // (off by default: measured slower with 8 streams sharing the chip, profiles/r01k_ab.txt)
+    static const uint32_t max_split = [] { const char *e = getenv("BPG_ROW_SPLIT"); return e ? (uint32_t)atoi(e) : 1u; }();
+    // (fixed-base jobs have one row per MSM: always split those)
+    const uint32_t msplit = p.fixed ? 64u : max_split;
+    uint32_t split = 1;
+    while ((uint32_t)p.rows * split < 256 && split < msplit && p.nseg_per_row / (split * 2) >= 64) split *= 2;
+    if (split == 1) {
+        hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
+                           (uint32_t)p.nseg_per_row, lgL, 1u, AS_GE(rows_dev_.p));
+    } else {
+        ge *parts = AS_GE(rows_dev_.p) + p.rows;
+        hipLaunchKernelGGL(k_row_reduce, dim3(p.rows * split), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
+                           (uint32_t)p.nseg_per_row, lgL, split, parts);
+        hipLaunchKernelGGL(k_row_final, dim3(nblk(p.rows, 64)), dim3(64), 0, st_, (const ge *)parts, (uint32_t)p.rows,
+                           split, AS_GE(rows_dev_.p));
+    }
     BPG_HIP(hipGetLastError());
     BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;
@@ -1534,19 +1585,62 @@ void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab
     BPG_HIP(hipGetLastError());
 }
 
+// Fixed-base window tables: tab[w * N + j] = 2^(16 w) P_j (affine Niels)
+__global__ __launch_bounds__(64) void k_wtab_build(const gen *__restrict__ gens, uint32_t N, gen *__restrict__ tab) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    gen g;
+    gen_load(g, gens + j);
+    gen_store(tab + j, g);
+    gec c;
+    gen_to_cached(c, g);
+    ge pw;
+    ge_from_cached(pw, c);
+    for (int w = 1; w < WTAB_W; w++) {
+        for (int k = 0; k < WTAB_C - 1; k++) ge_dbl_t<false>(pw, pw);
+        ge_dbl_t<true>(pw, pw);
+        gen e;
+        ge_to_niels(e, pw);
+        gen_store(tab + (size_t)w * N + j, e);
+    }
+}
+void launch_wtab_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st) {
+    hipLaunchKernelGGL(k_wtab_build, dim3(nblk(N, 64)), dim3(64), 0, st, AS_CGEN(gens), N, reinterpret_cast<gen *>(tab));
+    BPG_HIP(hipGetLastError());
+}
+
 // Output lane i < h1 of vector v (0 = G, 1 = H):
 //   out_i = P_i + sum_{t<3} c_t * P_{i + (t+1) h1}
-// with per-lane-range coefficient digits (signed radix 16, LSB first); no
-// doublings: every nonzero digit is one table read and one 7M madd.
-__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restrict__ Ap) {
-    const CombArgs &A = *Ap;
-    const uint32_t nb = (A.h1 + 63) / 64;
-    const uint32_t v = blockIdx.x >= nb ? 1 : 0;
-    const uint32_t i = (blockIdx.x - v * nb) * 64 + threadIdx.x;
-    if (i >= A.h1) return;
-    uint32_t r = 0;
+// with per-lane-range coefficient digits (signed radix 16); no doublings:
+// every nonzero digit is one table read and one 7M madd. The host flattens
+// the nonzero digits of each (vector, range) into an op list read with scalar
+// loads (blocks never straddle a range), and the table entry of op k+1 is in
+// flight while op k's addition runs.
+#define COMB_MAXSEG (2 * COMB_MAXRANGE)
+#define COMB_MAXOPS 192
+struct CombDev {
+    const void *gens[2];
+    const void *tab[2];
+    void *out[2];
+    uint32_t ntab, nseg;
+    uint32_t start[COMB_MAXSEG], end[COMB_MAXSEG], blk0[COMB_MAXSEG + 1], vec[COMB_MAXSEG], nops[COMB_MAXSEG];
+    // op: table row (w * 8 + m - 1, 9 bits) | t << 9 | neg << 11
+    uint16_t ops[COMB_MAXSEG][COMB_MAXOPS];
+};
+DEVI void comb_entry_load(uint4 (&q)[6], const uint4 *tab, uint32_t op, uint32_t ntab, uint32_t h1, uint32_t i) {
+    const uint32_t jj = i + ((op >> 9) & 3) * h1;
+    const uint4 *e = tab + ((size_t)(op & 511) * ntab + jj) * 6;
 #pragma unroll
-    for (int k = 1; k < COMB_MAXRANGE; k++) if (k < (int)A.nrange && i >= A.rstart[k]) r = k;
+    for (int u = 0; u < 6; u++) q[u] = e[u];
+}
+__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombDev *__restrict__ Ap) {
+    const CombDev &A = *Ap;
+    uint32_t b = blockIdx.x, sg = 0;
+    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
+    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
+    if (i >= A.end[sg]) return;
+    const uint32_t v = A.vec[sg], nops = A.nops[sg], ntab = A.ntab, h1 = A.ntab / 3;
+    const uint16_t *ops = A.ops[sg];
     const uint4 *tab = reinterpret_cast<const uint4 *>(A.tab[v]);
     ge acc;
     ge_identity(acc);
@@ -1555,27 +1649,15 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
         gen_load(p, reinterpret_cast<const gen *>(A.gens[v]) + i);
         ge_madd(acc, acc, p);
     }
-    for (int t = 0; t < 3; t++) {
-        const uint32_t jj = i + (uint32_t)t * A.h1;
-        const uint32_t *dw = reinterpret_cast<const uint32_t *>(A.dig[v][r][t]);
-        for (int w4 = 0; w4 < 16; w4++) {
-            const uint32_t packed = dw[w4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int d = (int)(int8_t)(packed >> (8 * k));
-                if (d == 0) continue;
-                const int w = 4 * w4 + k;
-                const int m = d < 0 ? -d : d;
-                const uint4 *e = tab + ((size_t)(w * 8 + m - 1) * A.ntab + jj) * 6;
-                uint4 q[6];
-#pragma unroll
-                for (int u = 0; u < 6; u++) q[u] = e[u];
-                gen p;
-                genp_unpack(p, q);
-                gen_cneg(p, d < 0);
-                ge_madd(acc, acc, p);
-            }
-        }
+    uint4 q[6];
+    if (nops) comb_entry_load(q, tab, ops[0], ntab, h1, i);
+    for (uint32_t k = 0; k < nops; k++) {
+        const uint32_t op = ops[k];
+        gen p;
+        genp_unpack(p, q);
+        if (k + 1 < nops) comb_entry_load(q, tab, ops[k + 1], ntab, h1, i);
+        gen_cneg(p, (op >> 11) & 1);
+        ge_madd(acc, acc, p);
     }
     gec out;
     ge_to_cached(out, acc);
@@ -1583,29 +1665,46 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
 }
 void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st) {
     if (!args.h1) return;
+    if (args.nrange < 1 || args.nrange > COMB_MAXRANGE) throw HipError(hipErrorInvalidValue, "comb ranges", __FILE__, __LINE__);
     if (!stage.dev) {
-        BPG_HIP(hipMalloc(&stage.dev, sizeof(CombArgs)));
-        BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombArgs), hipHostMallocDefault));
+        BPG_HIP(hipMalloc(&stage.dev, sizeof(CombDev)));
+        BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombDev), hipHostMallocDefault));
         BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
     } else {
         BPG_HIP(hipEventSynchronize(stage.copied));
     }
-    memcpy(stage.host, &args, sizeof(CombArgs));
-    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombArgs), hipMemcpyHostToDevice, st));
-    BPG_HIP(hipEventRecord(stage.copied, st));
-    const uint32_t nb = (args.h1 + 63) / 64;
-    // reads 4 level-0 points, writes 1 level-2 point per lane, G and H (SURVEY §8d);
-    // one 7M madd per nonzero digit (+ the base term and the cached output)
+    CombDev &D = *reinterpret_cast<CombDev *>(stage.host);
+    for (int v = 0; v < 2; v++) { D.gens[v] = args.gens[v]; D.tab[v] = args.tab[v]; D.out[v] = args.out[v]; }
+    D.ntab = args.ntab;
+    D.nseg = 0;
+    uint32_t blocks = 0;
     double fem = 0;
     for (uint32_t v = 0; v < 2; v++)
         for (uint32_t r = 0; r < args.nrange; r++) {
             const uint32_t lo = args.rstart[r], hi = r + 1 < args.nrange ? args.rstart[r + 1] : args.h1;
-            uint32_t nz = 0;
-            for (int t = 0; t < 3; t++) for (int w = 0; w < 64; w++) nz += args.dig[v][r][t][w] != 0;
-            fem += (double)(hi - lo) * (7.0 * (nz + 1) + 1.0);
+            if (hi <= lo) continue;
+            const uint32_t sg = D.nseg++;
+            D.start[sg] = lo; D.end[sg] = hi; D.vec[sg] = v; D.blk0[sg] = blocks;
+            blocks += nblk(hi - lo, 64);
+            uint32_t n = 0;
+            for (uint32_t t = 0; t < 3; t++)
+                for (uint32_t w = 0; w < 64; w++) {
+                    const int d = args.dig[v][r][t][w];
+                    if (!d) continue;
+                    const uint32_t m = (uint32_t)(d < 0 ? -d : d);
+                    D.ops[sg][n++] = (uint16_t)((w * 8 + m - 1) | (t << 9) | ((d < 0 ? 1u : 0u) << 11));
+                }
+            D.nops[sg] = n;
+            fem += (double)(hi - lo) * (7.0 * (n + 1) + 1.0);
         }
+    D.blk0[D.nseg] = blocks;
+    if (!blocks) return;
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombDev), hipMemcpyHostToDevice, st));
+    BPG_HIP(hipEventRecord(stage.copied, st));
+    // reads 4 level-0 points, writes 1 level-2 point per lane, G and H (SURVEY §8d);
+    // one 7M madd per nonzero digit (+ the base term and the cached output)
     ProfScope ps("ipp_comb_fold", 2.0 * args.h1 * (4 * 64 + 64), fem);
-    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, reinterpret_cast<const CombArgs *>(stage.dev));
+    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const CombDev *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }
 

@@ -77,6 +77,16 @@ int bpg_set_fold_pairs(int mode) {
     set_fold_pairs(mode);
     return 0;
 }
+int bpg_set_msm_affine(int mode) {
+    if (mode < -1 || mode > 1) return -1;
+    set_msm_affine(mode);
+    return 0;
+}
+int bpg_set_msm_fixed(int mode) {
+    if (mode < -1 || mode > 1) return -1;
+    set_msm_fixed(mode);
+    return 0;
+}
 int bpg_set_device(int device) {
     if (device < 0) return -1;
     g_device = device;

@@ -355,6 +355,14 @@ void pt_to_dev_niels(uint32_t w[32], const Point &p) {
     fe_to_w(w, ypx); fe_to_w(w + 10, ymx); fe_to_w(w + 20, t2d);
     w[30] = w[31] = 0;
 }
+void pt_to_dev_affine(uint32_t w[16], const Point &p) {
+    Fe t19, t3, zi, x, y;
+    fpow22501(t19, t3, p.Z); fsqn(t19, t19, 5); fmul(zi, t19, t3);   // Z^(p-2)
+    fmul(x, p.X, zi); fmul(y, p.Y, zi);
+    uint8_t b[32];
+    ftobytes(b, x); memcpy(w, b, 32);
+    ftobytes(b, y); memcpy(w + 8, b, 32);
+}
 void pt_from_dev_niels(Point &p, const uint32_t w[32]) {
     Fe ypx, ymx, two, t;
     fe_from_w(ypx, w); fe_from_w(ymx, w + 10);

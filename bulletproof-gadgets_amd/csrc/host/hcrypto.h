@@ -58,6 +58,7 @@ void pt_from_dev(Point &p, const uint32_t w[40]);   // device layout, dev_field.
 void pt_to_dev(uint32_t w[40], const Point &p);
 void pt_to_dev_cached(uint32_t w[40], const Point &p);   // (Y+X, Y-X, 2Z, 2dT)
 void pt_to_dev_niels(uint32_t w[32], const Point &p);    // affine (y+x, y-x, 2dxy)
+void pt_to_dev_affine(uint32_t w[16], const Point &p);   // affine (x, y), canonical words
 void pt_from_dev_niels(Point &p, const uint32_t w[32]);
 // signed radix-16 digits of the reduced scalar, LSB first, |e[i]| <= 8
 // (curve25519-dalek Scalar::to_radix_16)

@@ -84,11 +84,18 @@ void DeviceContext::ensure_gens(uint32_t N) {
         BPG_HIP(hipMemcpy(duni, uni.data(), uni.size(), hipMemcpyHostToDevice));
         launch_gens_map(duni, which ? nH : nG, cap, 0);
     }
+    AffD *aG = nullptr, *aH = nullptr;
+    BPG_HIP(hipMalloc(&aG, (size_t)cap * sizeof(AffD)));
+    BPG_HIP(hipMalloc(&aH, (size_t)cap * sizeof(AffD)));
+    launch_to_affine(nG, aG, cap, 0);
+    launch_to_affine(nH, aH, cap, 0);
     BPG_HIP(hipDeviceSynchronize());
     (void)hipFree(duni);
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
-    G = nG; H = nH; gens_cap = cap;
+    if (Ga) (void)hipFree(Ga);
+    if (Ha) (void)hipFree(Ha);
+    G = nG; H = nH; Ga = aG; Ha = aH; gens_cap = cap;
 }
 
 static std::atomic<int> g_fold_tables(-1);
@@ -106,6 +113,51 @@ static bool fold_pairs_enabled() {
     if (m >= 0) return m != 0;
     const char *e = getenv("BPG_FOLD_PAIRS");
     return !(e && e[0] == '0');
+}
+static std::atomic<int> g_msm_affine(-1);
+void set_msm_affine(int mode) { g_msm_affine = mode; }
+static bool msm_affine_enabled() {
+    int m = g_msm_affine;
+    if (m >= 0) return m != 0;
+    const char *e = getenv("BPG_MSM_AFFINE");
+    return e && e[0] == '1';
+}
+static std::atomic<int> g_msm_fixed(-1);
+void set_msm_fixed(int mode) { g_msm_fixed = mode; }
+static bool msm_fixed_enabled() {
+    int m = g_msm_fixed;
+    if (m >= 0) return m != 0;
+    const char *e = getenv("BPG_MSM_FIXED");
+    return e && e[0] == '1';
+}
+WinTables::~WinTables() {
+    if (G || H) (void)hipSetDevice(device);
+    if (G) (void)hipFree(G);
+    if (H) (void)hipFree(H);
+}
+std::shared_ptr<WinTables> DeviceContext::ensure_wtab(uint32_t N) {
+    if (N < 2 || !msm_fixed_enabled()) return nullptr;
+    ensure_gens(N);
+    std::lock_guard<std::mutex> lk(mu);
+    if (wtab && wtab->N >= N) return wtab;
+    BPG_HIP(hipSetDevice(device));
+    wtab.reset();
+    const size_t bytes = (size_t)WTAB_W * N * sizeof(NielsD);   // per vector
+    size_t free_b = 0, total_b = 0;
+    BPG_HIP(hipMemGetInfo(&free_b, &total_b));
+    if (2 * bytes + ((size_t)16 << 30) > free_b) return nullptr;
+    std::shared_ptr<WinTables> t(new WinTables());
+    t->device = device;
+    t->N = N;
+    if (hipMalloc((void **)&t->G, bytes) != hipSuccess || hipMalloc((void **)&t->H, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    launch_wtab_build(G, N, t->G, 0);
+    launch_wtab_build(H, N, t->H, 0);
+    BPG_HIP(hipDeviceSynchronize());
+    wtab = t;
+    return wtab;
 }
 CombTables::~CombTables() {
     if (tabG || tabH) (void)hipSetDevice(device);
@@ -358,6 +410,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
         P->V.resize((size_t)m * 32);
         if (m) gpu_pedersen(device, P->v, P->vb, P->V.data());
         DeviceContext::get(device).ensure_comb(P->N);   // circuit-independent, outside any timed region
+        DeviceContext::get(device).ensure_wtab(P->N);
     }
     return P;
 }
@@ -571,12 +624,21 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G> (blinding terms added on the host)
     PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
     MsmPlan pA{}, pS{};
+    // MSM bases for the level-0 generators
+    // (fixed-base window tables when present: all windows of an MSM share one
+    // row of buckets; else affine or affine-Niels generators)
+    std::shared_ptr<WinTables> wt = ctx.ensure_wtab(N);
+    const bool aff = !wt && msm_affine_enabled();
+    const void *G0m = wt ? (const void *)wt->G : aff ? (const void *)ctx.Ga : (const void *)ctx.G;
+    const void *H0m = wt ? (const void *)wt->H : aff ? (const void *)ctx.Ha : (const void *)ctx.H;
+    const int fmt0 = aff ? MSM_AFFINE : MSM_NIELS;
+    const uint32_t ws0 = wt ? wt->N : 0;   // window stride of the level-0 bases
     if (n) {
-        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), ctx.G, n, 0},
-                          {as<ScD>(const_cast<DBuf &>(cs.aR)), ctx.H, n, 0},
-                          {as<ScD>(const_cast<DBuf &>(cs.aO)), ctx.G, n, 1}};
+        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0m, n, 0, ws0},
+                          {as<ScD>(const_cast<DBuf &>(cs.aR)), H0m, n, 0, ws0},
+                          {as<ScD>(const_cast<DBuf &>(cs.aO)), G0m, n, 1, ws0}};
         int ph = ws.prof_begin("msm_commit", 3.0 * n * (64 + 32));
-        pA = ws.msm->enqueue(segA, 3, 2, rowsA, MSM_NIELS);
+        pA = ws.msm->enqueue(segA, 3, 2, rowsA, fmt0);
         ws.prof_end(ph);
     }
     // s_L | s_R: raw 64-byte draws -> device, reduced mod l there
@@ -591,9 +653,9 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         }
         launch_wide_reduce(wd, n, as<ScD>(ws.sL), st);
         launch_wide_reduce(wd + 64 * (size_t)n, n, as<ScD>(ws.sR), st);
-        MsmSeg segS[2] = {{as<ScD>(ws.sL), ctx.G, n, 0}, {as<ScD>(ws.sR), ctx.H, n, 0}};
+        MsmSeg segS[2] = {{as<ScD>(ws.sL), G0m, n, 0, ws0}, {as<ScD>(ws.sR), H0m, n, 0, ws0}};
         int ph = ws.prof_begin("msm_commit", 2.0 * n * (64 + 32));
-        pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
+        pS = ws.msm->enqueue(segS, 2, 1, rowsS, fmt0);
         ws.prof_end(ph);
     }
     ws.sync();
@@ -697,16 +759,18 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     Point Qp; mul_B(Qp, wch);
     // Q in both base formats: cached for jobs over folded generators, affine
     // Niels for jobs over the level-0 generators
-    ws.Q.grow(sizeof(PtD) + sizeof(NielsD));
+    ws.Q.grow(sizeof(PtD) + sizeof(NielsD) + sizeof(AffD));
     {
-        uint8_t qb[sizeof(PtD) + sizeof(NielsD)];
+        uint8_t qb[sizeof(PtD) + sizeof(NielsD) + sizeof(AffD)];
         pt_to_dev_cached(reinterpret_cast<uint32_t *>(qb), Qp);
         pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD)), Qp);
+        pt_to_dev_affine(reinterpret_cast<uint32_t *>(qb + sizeof(PtD) + sizeof(NielsD)), Qp);
         memcpy(ws.small_host + 3000, qb, sizeof(qb));
         BPG_HIP(hipMemcpyAsync(ws.Q.p, ws.small_host + 3000, sizeof(qb), hipMemcpyHostToDevice, st));
     }
     const PtD *Qc = as<PtD>(ws.Q);
     const NielsD *Qn = reinterpret_cast<const NielsD *>(as<uint8_t>(ws.Q) + sizeof(PtD));
+    const AffD *Qa = reinterpret_cast<const AffD *>(as<uint8_t>(ws.Q) + sizeof(PtD) + sizeof(NielsD));
     ws.a.grow((size_t)N * sizeof(ScD) + 64);
     ws.b.grow((size_t)N * sizeof(ScD) + 64);
     launch_lr_eval(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0), as<ScD>(ws.r1),
@@ -744,40 +808,56 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         A.lamG1 = mont(lam); A.lamGu = mont(lam * u);
         A.muH1 = mont(mu); A.muHu = mont(mu * u);
         ScD *ms = as<ScD>(ws.mscal);
-        const void *Qb = gfmt == MSM_NIELS ? (const void *)Qn : (const void *)Qc;
-        const size_t ps = gfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
+        // MSM bases: the level-0 generators in the MSM format, else Ghat/Hhat
+        const int mfmt = cur < 0 ? fmt0 : MSM_CACHED;
+        const void *Gm = cur < 0 ? G0m : Gh, *Hm = cur < 0 ? H0m : Hh;
+        const void *Qb = mfmt == MSM_NIELS ? (const void *)Qn : mfmt == MSM_AFFINE ? (const void *)Qa : (const void *)Qc;
+        const size_t ps = mfmt == MSM_NIELS ? sizeof(NielsD) : mfmt == MSM_AFFINE ? sizeof(AffD) : sizeof(PtD);
         auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
+        // over window tables, c_L Q and c_R Q leave the job: Q = w B, so they
+        // are (c w) B on the host
+        const uint32_t wsr = cur < 0 ? ws0 : 0;
         MsmSeg seg[10];
         int nseg;
         const bool lazy = pend;
+        const size_t hh = h;
+        const ScD *cLR;   // c_L, c_R on the device
         if (lazy) {
             const uint32_t h0 = 2 * h;
             LazyArgs Z;
             Z.h0 = h0;
             Z.rGa = mont(rho_p[0]); Z.rGb = mont(rho_p[1]); Z.rHa = mont(rho_p[2]); Z.rHb = mont(rho_p[3]);
             launch_ipp_prep_lazy(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
-            const size_t hh = h;
-            MsmSeg sl[10] = {{ms, at(Gh, h), h, 0}, {ms + hh, at(Gh, h + h0), h, 0}, {ms + 2 * hh, Hh, h, 0},
-                             {ms + 3 * hh, at(Hh, h0), h, 0}, {ms + 8 * hh, Qb, 1, 0},
-                             {ms + 4 * hh, Gh, h, 1}, {ms + 5 * hh, at(Gh, h0), h, 1}, {ms + 6 * hh, at(Hh, h), h, 1},
-                             {ms + 7 * hh, at(Hh, h + h0), h, 1}, {ms + 8 * hh + 1, Qb, 1, 1}};
-            std::copy(sl, sl + 10, seg);
-            nseg = 10;
+            MsmSeg sl[10] = {{ms, at(Gm, h), h, 0, wsr}, {ms + hh, at(Gm, h + h0), h, 0, wsr}, {ms + 2 * hh, Hm, h, 0, wsr},
+                             {ms + 3 * hh, at(Hm, h0), h, 0, wsr}, {ms + 8 * hh, Qb, 1, 0},
+                             {ms + 4 * hh, Gm, h, 1, wsr}, {ms + 5 * hh, at(Gm, h0), h, 1, wsr},
+                             {ms + 6 * hh, at(Hm, h), h, 1, wsr}, {ms + 7 * hh, at(Hm, h + h0), h, 1, wsr},
+                             {ms + 8 * hh + 1, Qb, 1, 1}};
+            nseg = 0;
+            for (const MsmSeg &g : sl) if (!(wsr && g.count == 1 && g.base == Qb)) seg[nseg++] = g;
+            cLR = ms + 8 * hh;
         } else {
             launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-            const size_t hh = h;
-            MsmSeg sl[6] = {{ms, at(Gh, h), h, 0}, {ms + hh, Hh, h, 0}, {ms + 4 * hh, Qb, 1, 0},
-                            {ms + 2 * hh, Gh, h, 1}, {ms + 3 * hh, at(Hh, h), h, 1}, {ms + 4 * hh + 1, Qb, 1, 1}};
-            std::copy(sl, sl + 6, seg);
-            nseg = 6;
+            MsmSeg sl[6] = {{ms, at(Gm, h), h, 0, wsr}, {ms + hh, Hm, h, 0, wsr}, {ms + 4 * hh, Qb, 1, 0},
+                            {ms + 2 * hh, Gm, h, 1, wsr}, {ms + 3 * hh, at(Hm, h), h, 1, wsr},
+                            {ms + 4 * hh + 1, Qb, 1, 1}};
+            nseg = 0;
+            for (const MsmSeg &g : sl) if (!(wsr && g.count == 1 && g.base == Qb)) seg[nseg++] = g;
+            cLR = ms + 4 * hh;
         }
         int ph = ws.prof_begin("msm_ipp", ((lazy ? 8.0 : 4.0) * h + 2) * (64 + 32));
-        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, gfmt);
+        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, mfmt);
         ws.prof_end(ph);
+        if (wsr) BPG_HIP(hipMemcpyAsync(ws.small_host + 1020, cLR, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
         ws.sync();
         Point Lp, Rp;
         combine_rows(Lp, rowsLR, pl.W, pl.c);
         combine_rows(Rp, rowsLR + pl.W, pl.W, pl.c);
+        if (wsr) {
+            Point q;
+            mul_B(q, from_dev(ws.small_host[1020]) * wch); pt_add(Lp, Lp, q);
+            mul_B(q, from_dev(ws.small_host[1021]) * wch); pt_add(Rp, Rp, q);
+        }
         uint8_t *cl = LRc.data() + 64 * (size_t)k, *cr = cl + 32;
         ristretto_compress(cl, Lp);
         ristretto_compress(cr, Rp);

@@ -32,11 +32,20 @@ struct CombTables {
     size_t bytes = 0;
     ~CombTables();
 };
+// Fixed-base window tables of G and H (DESIGN.md "Fixed-base MSMs"):
+// [w * N + j] = 2^(16 w) P_j for w < 16, affine Niels, 4 GB at N = 2^20.
+struct WinTables {
+    int device = 0;
+    uint32_t N = 0;
+    dev::NielsD *G = nullptr, *H = nullptr;
+    ~WinTables();
+};
 struct DeviceContext {
     int device = 0;
     std::mutex mu;
     uint32_t gens_cap = 0;
     dev::NielsD *G = nullptr, *H = nullptr;   // gens_cap points each, affine Niels
+    dev::AffD *Ga = nullptr, *Ha = nullptr;   // the same points as affine (x, y): 64-B MSM gathers
     PtD *tabB = nullptr, *tabBb = nullptr;
     PtD *Bb = nullptr;                  // B_blinding as a device point
     std::shared_ptr<CombTables> comb;   // for one N at a time
@@ -46,11 +55,23 @@ struct DeviceContext {
     // disabled (bpg_set_fold_tables / BPG_FOLD_TABLES=0), N < 8, or when they
     // would not fit in free HBM with room left for workspaces.
     std::shared_ptr<CombTables> ensure_comb(uint32_t N);
+    std::shared_ptr<WinTables> wtab;
+    // Window tables for N generators (null when disabled by bpg_set_msm_fixed /
+    // BPG_MSM_FIXED=0 or when they would not fit in free HBM)
+    std::shared_ptr<WinTables> ensure_wtab(uint32_t N);
 };
 // -1 auto (env BPG_FOLD_TABLES, default on), 0 off, 1 on
 void set_fold_tables(int mode);
 // -1 auto (env BPG_FOLD_PAIRS, default on), 0 off, 1 on
 void set_fold_pairs(int mode);
+// MSM base format for the level-0 generators: -1 auto (env BPG_MSM_AFFINE,
+// default off: measured no throughput gain, profiles/r01j_ab.txt), 0 affine
+// Niels (128 B, 7M adds), 1 affine (64 B, 9M adds)
+void set_msm_affine(int mode);
+// level-0 MSMs over fixed-base window tables: -1 auto (env BPG_MSM_FIXED,
+// default off: 11% slower, the 4 GB of tables defeat the cache reuse of the
+// 256 MB of generators, profiles/r01l_ab.txt), 0 off, 1 on
+void set_msm_fixed(int mode);
 
 // Flattened circuit resident on the device (inputs in HBM before timing).
 struct PreparedCS {

@@ -94,6 +94,19 @@ int bpg_set_fold_tables(int mode);
  * either way. */
 int bpg_set_fold_pairs(int mode);
 
+/* Added: MSM base format of the generators (process-wide). mode 1: affine
+ * (x, y), 64-B gathers and 9M additions; mode 0: affine Niels, 128-B gathers
+ * and 7M additions; -1: automatic (affine Niels; env BPG_MSM_AFFINE=1 selects affine).
+ * Proof bytes are identical either way. */
+int bpg_set_msm_affine(int mode);
+
+/* Added: fixed-base window tables for the MSMs over the generators
+ * (process-wide). mode 1: 2^(16w) G_j, 2^(16w) H_j for w < 16 resident in HBM
+ * (~4 KB x N per device), every window of an MSM shares one row of buckets;
+ * mode 0: one bucket row per window; -1: automatic (mode 0; env
+ * BPG_MSM_FIXED=1 selects tables). Proof bytes are identical either way. */
+int bpg_set_msm_fixed(int mode);
+
 /* ------------------------------------------------------------------------ */
 /* 2. Inner operator ABI: the flattened constraint system                     */
 /* ------------------------------------------------------------------------ */

@@ -70,14 +70,19 @@ def test_full_size_verify_and_strategies(bpg, ctx, W, cfg):
     proofs = []
     # (comb tables, round-pair folds): table pass + Straus pair folds, Straus
     # pair folds only, one variable-base fold per round
-    for tables, pairs in ((1, 1), (0, 1), (0, 0)):
+    # and affine / affine-Niels / window-table generator bases in the MSMs
+    for tables, pairs, aff, fixed in ((1, 1, 0, 1), (0, 1, 1, 0), (0, 0, 0, 0)):
         assert lib.bpg_set_fold_tables(tables) == 0
         assert lib.bpg_set_fold_pairs(pairs) == 0
+        assert lib.bpg_set_msm_affine(aff) == 0
+        assert lib.bpg_set_msm_fixed(fixed) == 0
         try:
             p, V = ctx.r1cs_prove(b"scale", syn.view, ent)
         finally:
             lib.bpg_set_fold_tables(-1)
             lib.bpg_set_fold_pairs(-1)
+            lib.bpg_set_msm_affine(-1)
+            lib.bpg_set_msm_fixed(-1)
         proofs.append(p)
     assert proofs[0] == proofs[1] == proofs[2]
     proof = proofs[0]
