@@ -138,7 +138,7 @@ def main():
     for s in range(a.warmup):
         prep.prove_batch(b"bench", entropies(1000 + s), threads)
     L = bpg.lib()
-    L.bpg_profile_enable(1)
+    L.bpg_profile_enable(0 if os.environ.get("BENCH_LIVE_TIMING") == "0" else 1)
     L.bpg_kernel_stats_reset()
 
     def barrier():
@@ -147,12 +147,15 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    c0 = os.times()
     t0 = time.perf_counter()
     proofs = []
     for s in range(a.steps):
         proofs.append(prep.prove_batch(b"bench", entropies(s), threads))
     barrier()
     dt = time.perf_counter() - t0
+    c1 = os.times()
+    host_busy = ((c1.user - c0.user) + (c1.system - c0.system)) / dt   # host cores kept busy by this rank
     L.bpg_profile_enable(0)
     if dist is not None:
         dt = D.max_over_ranks(dt)
@@ -218,6 +221,7 @@ def main():
         "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
                    "proofs_per_step_per_gpu": batch, "host_threads_per_gpu": threads,
                    "parallelism": "independent proofs per GPU (%d ranks)" % world},
+        "host_cores_busy": round(host_busy, 2),
         "latency_ms_single_proof": round(single_ms, 1),
         "phase_ms_single_proof": single_phases,
         "roofline": roof,

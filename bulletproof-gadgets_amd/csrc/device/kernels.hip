@@ -234,6 +234,7 @@ struct SegTab {
     uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t row0[MSM_MAXSEG];
     uint32_t wstride[MSM_MAXSEG];   // fixed-base jobs: points between window tables
+    uint32_t moff[MSM_MAXSEG], mtot[MSM_MAXSEG];   // first point and point count of the segment's MSM
     int n;
 };
 #define MSM_VAL_G 0x00ffffffu       // val = sign << 31 | window << 24 (fixed-base) | point
@@ -244,10 +245,13 @@ DEVI int seg_of(const SegTab &T, uint32_t g) {
     return si;
 }
 
-// signed c-bit windows; key = (row + w * wrow) * half + (|d| - 1), val = point | sign << 31
-// (wrow = 1: one row per window; wrow = 0, fixed-base: one row per MSM and the
-// window goes into the value)
-__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t wrow, uint32_t half, uint32_t invalid,
+// Signed c-bit windows. Entry of (point g, window w): key = row << c | slot,
+// slot = |d| - 1 (< half) or half for a zero digit (a trash slot whose run is
+// skipped), val = point | sign << 31. Rows are numbered window-major (row =
+// w * nmsm + msm; fixed-base jobs: row = msm, window in bits 24.. of val), so
+// with the entries laid out [w][g] and segments ordered by MSM, the key array
+// is already grouped by row: the sort only orders each row by slot.
+__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t fixed, uint32_t half,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
@@ -255,7 +259,7 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t wr
     sc k;
     sc_load(k, T.scal[si] + (g - T.gofs[si]));
     uint32_t carry = 0, mask = (1u << c) - 1, full = 1u << c;
-    uint32_t row = T.row0[si];
+    const uint32_t m = T.row0[si];
     for (int w = 0; w < W; w++) {
         int bit = w * c;
         int lo = bit >> 5, sh = bit & 31;
@@ -263,18 +267,22 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t wr
         if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
         uint32_t d = (uint32_t)(x >> sh) & mask;
         d += carry;
-        const uint32_t rw = row + (uint32_t)w * wrow;
-        uint32_t key = invalid, val = g | (wrow ? 0u : (uint32_t)w << 24);
+        const uint32_t row = fixed ? m : (uint32_t)w * nmsm + m;
+        uint32_t slot = half, val = g | (fixed ? (uint32_t)w << 24 : 0u);
         if (d > half) {
             uint32_t mag = full - d;
             carry = 1;
-            if (mag) { key = rw * half + (mag - 1); val |= 0x80000000u; }
+            if (mag) { slot = mag - 1; val |= 0x80000000u; }
         } else {
             carry = 0;
-            if (d) key = rw * half + (d - 1);
+            if (d) slot = d - 1;
         }
-        keys[(size_t)w * total + g] = key;
-        vals[(size_t)w * total + g] = val;
+        // rows contiguous: [w][g] (one row per window and MSM) or, fixed-base,
+        // [msm][w][g of that MSM]
+        const size_t pos = fixed ? (size_t)T.moff[si] * W + (size_t)w * T.mtot[si] + (g - T.moff[si])
+                                 : (size_t)w * total + g;
+        keys[pos] = row << c | slot;
+        vals[pos] = val;
     }
 }
 
@@ -288,17 +296,19 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t wr
 // ---------------------------------------------------------------------------
 // Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
 #define RS_MAXBINS 256
+#define RS_MAXTILES (2048 + 4096)   // tiles of a job: <= 2048 full ones + one partial per row
 #define RS_BLOCK 256
 #define RS_ROUNDS 8
 #define RS_ITER (RS_BLOCK * RS_ROUNDS)
 template <int RS_BITS>
-__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict__ keys, uint32_t E, int shift,
-                                                      uint32_t tile, uint32_t nb, uint32_t *__restrict__ hist) {
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict__ keys, int shift,
+                                                      const uint32_t *__restrict__ tiles, uint32_t nb,
+                                                      uint32_t *__restrict__ hist) {
     constexpr uint32_t RS_BINS = 1u << RS_BITS;
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * tile, t1 = (t0 + tile < E) ? t0 + tile : E;
+    const uint64_t t0 = tiles[5 * blockIdx.x], t1 = tiles[5 * blockIdx.x + 1];
     for (uint64_t i = t0 + threadIdx.x; i < t1; i += RS_BLOCK) atomicAdd(&h[(keys[i] >> shift) & (RS_BINS - 1)], 1u);
     __syncthreads();
     if (threadIdx.x < RS_BINS) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
@@ -334,7 +344,7 @@ __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist,
 // write consecutive addresses.
 template <int RS_BITS>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
-                                                         uint32_t E, int shift, uint32_t tile, uint32_t nb,
+                                                         int shift, const uint32_t *__restrict__ tiles, uint32_t nb,
                                                          const uint32_t *__restrict__ hist,
                                                          const uint32_t *__restrict__ total,
                                                          uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
@@ -344,8 +354,18 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
     __shared__ uint32_t lk[RS_ITER], lv[RS_ITER];
     const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull);
-    // digit offsets: exclusive scan of the digit totals, plus this block's column offset
-    if (t < RS_BINS) lstart[t] = total[t];
+    // Segmented by row: this tile's row occupies tiles [r0, r1) and elements
+    // from rstart; digit offsets = rstart + exclusive scan of the row's digit
+    // counts + the count of the digit in the row's earlier tiles (hist holds
+    // the exclusive prefix over all tiles per digit).
+    const uint32_t *TL = tiles + 5 * blockIdx.x;
+    const uint32_t r0 = TL[2], r1 = TL[3], rstart = TL[4];
+    uint32_t p0 = 0, cr = 0;
+    if (t < RS_BINS) {
+        p0 = hist[t * nb + r0];
+        cr = (r1 < nb ? hist[t * nb + r1] : total[t]) - p0;
+        lstart[t] = cr;
+    }
     __syncthreads();
     for (uint32_t d = 1; d < RS_BINS; d <<= 1) {
         uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
@@ -353,8 +373,8 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
         if (t < RS_BINS) lstart[t] += a;
         __syncthreads();
     }
-    if (t < RS_BINS) base[t] = lstart[t] - total[t] + hist[t * nb + blockIdx.x];
-    const uint64_t t0 = (uint64_t)blockIdx.x * tile, t1 = (t0 + tile < E) ? t0 + tile : E;
+    if (t < RS_BINS) base[t] = rstart + lstart[t] - cr + (hist[t * nb + blockIdx.x] - p0);
+    const uint64_t t0 = TL[0], t1 = TL[1];
     for (uint64_t it = t0; it < t1; it += RS_ITER) {
         uint32_t *cz = &cnt[0][0][0];
         for (uint32_t j = t; j < RS_ROUNDS * (RS_BLOCK / 64) * RS_BINS; j += RS_BLOCK) cz[j] = 0;
@@ -430,6 +450,9 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
 // ---------------------------------------------------------------------------
 #define RBK_FILL 0x80000000u
 #define RBK_KEY(x) ((x) & 0x7fffffffu)
+// bucket of key row << c | slot (slot < half = 2^(c-1); slot == half: trash)
+DEVI uint32_t rbk_bucket(uint32_t key, int c) { return (key >> c) * (1u << (c - 1)) + (key & ((1u << (c - 1)) - 1)); }
+DEVI bool rbk_trash(uint32_t key, int c) { return (key >> (c - 1)) & 1u; }
 DEVI uint32_t rbk_lds(uint32_t j) { return j + j / RBK_T; }
 DEVI void rbk_stage(uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t base, uint64_t E, uint32_t invalid) {
     for (uint32_t k = threadIdx.x; k < RBK_CHUNK; k += RBK_BLOCK) {
@@ -464,7 +487,7 @@ template <bool FIRST, int FMT>
 __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         const ge *__restrict__ pin, SegTab T, uint64_t E,
-                                                        uint32_t invalid, uint32_t *__restrict__ kout,
+                                                        uint32_t invalid, int cw, uint32_t *__restrict__ kout,
                                                         ge *__restrict__ pout, ge *__restrict__ buckets,
                                                         uint8_t *__restrict__ bflag) {
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
@@ -494,7 +517,7 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restri
     ge acc;
     ge_identity(acc);
     typename BaseOf<FMT>::T pnext;
-    if (FIRST) msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T)]);
+    if (FIRST && !rbk_trash(first, cw)) msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T)]);
     for (uint32_t i = 0; i < RBK_T; i++) {
         const uint32_t x = sk[rbk_lds(t * RBK_T + i)];
         const uint32_t k = RBK_KEY(x);
@@ -502,19 +525,25 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restri
         if (k != cur) {
             if (!head_done) {
                 if (open_start) { ko[0] = cur | (real ? 0u : RBK_FILL); if (real) ge_store(po, acc); }
-                else { if (real) { ge_store(buckets + cur, acc); bflag[cur] = 1; } ko[0] = cur | RBK_FILL; }
+                else { if (real) { ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1; } ko[0] = cur | RBK_FILL; }
                 head_done = true;
             } else if (real) {
-                ge_store(buckets + cur, acc); bflag[cur] = 1;
+                ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1;
             }
             cur = k; real = false;
             ge_identity(acc);
         }
         if (FIRST) {
+            // the base of entry i + 1 is in flight while entry i is added;
+            // zero digits (trash, sorted to the end of their row) are never added
+            const bool trash = rbk_trash(k, cw);
             typename BaseOf<FMT>::T p = pnext;
             const uint32_t v = sv[rbk_lds(t * RBK_T + i)];
-            if (i + 1 < RBK_T && RBK_KEY(sk[rbk_lds(t * RBK_T + i + 1)]) != invalid)
-                msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T + i + 1)]);
+            if (i + 1 < RBK_T) {
+                const uint32_t kn = RBK_KEY(sk[rbk_lds(t * RBK_T + i + 1)]);
+                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T + i + 1)]);
+            }
+            if (trash) continue;
             msm_add_loaded(acc, p, v >> 31);
             real = true;
         } else if (!(x & RBK_FILL)) {
@@ -526,20 +555,20 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restri
     const bool tail_open = nk == cur;
     if (!head_done) {            // one run in the chunk
         if (open_start || tail_open) { ko[0] = cur | (real ? 0u : RBK_FILL); if (real) ge_store(po, acc); }
-        else { if (real) { ge_store(buckets + cur, acc); bflag[cur] = 1; } ko[0] = cur | RBK_FILL; }
+        else { if (real) { ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1; } ko[0] = cur | RBK_FILL; }
         ko[1] = cur | RBK_FILL;
     } else if (tail_open) {
         ko[1] = cur | (real ? 0u : RBK_FILL);
         if (real) ge_store(po + 1, acc);
     } else {
-        if (real) { ge_store(buckets + cur, acc); bflag[cur] = 1; }
+        if (real) { ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1; }
         ko[1] = cur | RBK_FILL;
     }
 }
 // After the last pass: the head slot of each run sums the run's real pieces
 // and owns the bucket (serial; long only for giant runs of structured digits).
 __global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
-                                                  uint64_t E, uint32_t invalid, ge *__restrict__ buckets,
+                                                  uint64_t E, uint32_t invalid, int cw, ge *__restrict__ buckets,
                                                   uint8_t *__restrict__ bflag) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= E) return;
@@ -554,7 +583,7 @@ __global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ k
         ge_add(acc, acc, p);
         real = true;
     }
-    if (real) { ge_store(buckets + k, acc); bflag[k] = 1; }
+    if (real) { ge_store(buckets + rbk_bucket(k, cw), acc); bflag[rbk_bucket(k, cw)] = 1; }
 }
 // Window rows from buckets: R_row = sum_b (b+1) S_b over the half buckets.
 // Level 1 (thread per segment of L buckets): A_s = sum_j (j+1) S_{sL+j} and
@@ -599,9 +628,13 @@ DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {   // k * p, k < 2^8
     }
     r = acc;
 }
+// Rows are numbered window-major (row = w * nmsm + msm); results land at
+// msm * W + w, the layout the host combine reads (with split > 1 the block
+// parts stay in row order for k_row_final).
+DEVI uint32_t row_perm(uint32_t row, uint32_t nmsm, uint32_t W) { return (row % nmsm) * W + row / nmsm; }
 __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
-                                                    uint32_t nseg, int lgL, uint32_t split,
-                                                    ge *__restrict__ parts) {
+                                                    uint32_t nseg, int lgL, uint32_t split, uint32_t nmsm,
+                                                    uint32_t W, ge *__restrict__ parts) {
     __shared__ ge sh[256];
     const uint32_t row = blockIdx.x / split, j = blockIdx.x % split, t = threadIdx.x;
     const uint32_t M = nseg / split, s0 = j * M;
@@ -657,16 +690,19 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
             ge_store(&sh[t], a);
         }
     }
-    if (t == 0) { ge r; ge_load(r, &sh[0]); ge_store(parts + blockIdx.x, r); }
+    if (t == 0) {
+        ge r; ge_load(r, &sh[0]);
+        ge_store(parts + (split == 1 ? row_perm(blockIdx.x, nmsm, W) : blockIdx.x), r);
+    }
 }
 __global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ parts, uint32_t rows, uint32_t split,
-                                                  ge *__restrict__ rows_out) {
+                                                  uint32_t nmsm, uint32_t W, ge *__restrict__ rows_out) {
     const uint32_t row = blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= rows) return;
     ge acc, p;
     ge_load(acc, parts + (size_t)row * split);
     for (uint32_t j = 1; j < split; j++) { ge_load(p, parts + (size_t)row * split + j); ge_add(acc, acc, p); }
-    ge_store(rows_out + row, acc);
+    ge_store(rows_out + row_perm(row, nmsm, W), acc);
 }
 
 static int msm_window(uint64_t total) {
@@ -680,7 +716,9 @@ static int msm_window(uint64_t total) {
 }
 
 MsmEngine::~MsmEngine() {
-    DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_,
+    if (tiles_ev_) (void)hipEventDestroy(tiles_ev_);
+    if (tiles_host_) (void)hipHostFree(tiles_host_);
+    DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_,
                     &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &bflag_, &segacc_, &rows_dev_};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -698,7 +736,7 @@ void DBuf::grow(size_t need) {
 void MsmEngine::reserve(const MsmPlan &p) {
     size_t kb = p.E0 * 4;
     keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
-    sort_tmp_.grow((size_t)RS_MAXBINS * 2049 * 4 + 256);    // radix-sort block histograms + totals
+    sort_tmp_.grow((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256);   // radix-sort tile histograms + totals
     rk_a_.grow(p.capE * 4); rp_a_.grow(p.capE * sizeof(ge));
     rk_b_.grow(p.capE * 4 / 4 + 1024); rp_b_.grow((p.capE / 4 + 256) * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
@@ -707,30 +745,29 @@ void MsmEngine::reserve(const MsmPlan &p) {
     rows_dev_.grow((size_t)p.rows * 257 * sizeof(ge));   // rows + per-block parts (split <= 256)
 }
 
-// sort (keys, vals) -> sorted pairs; returns which buffers hold them
-static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2, uint64_t E, int key_bits,
-                       uint32_t *hist, hipStream_t st) {
-    if (E < 2) return;
-    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (E + 4095) / 4096));
-    uint64_t tile = (E + nb - 1) / nb;
-    tile = (tile + RS_ITER - 1) / RS_ITER * RS_ITER;
+// Sort (keys, vals) by the low key_bits within each row (tiles never straddle
+// a row; tiles_dev: nt x {start, end, first tile of the row, one past its last
+// tile, row start}); swaps the buffer pointers to the sorted pair.
+static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2, int key_bits, const uint32_t *tiles,
+                       uint32_t nt, uint32_t *hist, hipStream_t st) {
+    if (!nt || key_bits < 1) return;
     // 8-bit digits only where they save a pass (their scatter costs more LDS)
     static const bool sort8 = [] { const char *e = getenv("BPG_SORT8"); return !(e && e[0] == '0'); }();
     const int bits = sort8 && (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
     const uint32_t bins = 1u << bits;
-    uint32_t *total = hist + (size_t)bins * nb;
+    uint32_t *total = hist + (size_t)bins * nt;
     for (int shift = 0; shift < key_bits; shift += bits) {
         if (bits == 8)
-            hipLaunchKernelGGL(k_rs_hist<8>, dim3(nb), dim3(RS_BLOCK), 0, st, k, (uint32_t)E, shift, (uint32_t)tile, nb, hist);
+            hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         else
-            hipLaunchKernelGGL(k_rs_hist<7>, dim3(nb), dim3(RS_BLOCK), 0, st, k, (uint32_t)E, shift, (uint32_t)tile, nb, hist);
-        hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nb, total);
+            hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
+        hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nt, total);
         if (bits == 8)
-            hipLaunchKernelGGL(k_rs_scatter<8>, dim3(nb), dim3(RS_BLOCK), 0, st, k, v, (uint32_t)E, shift, (uint32_t)tile,
-                               nb, hist, total, k2, v2);
+            hipLaunchKernelGGL(k_rs_scatter<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist, total,
+                               k2, v2);
         else
-            hipLaunchKernelGGL(k_rs_scatter<7>, dim3(nb), dim3(RS_BLOCK), 0, st, k, v, (uint32_t)E, shift, (uint32_t)tile,
-                               nb, hist, total, k2, v2);
+            hipLaunchKernelGGL(k_rs_scatter<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist, total,
+                               k2, v2);
         std::swap(k, k2);
         std::swap(v, v2);
     }
@@ -763,18 +800,31 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     p.nmsm = nmsm;
     p.rows = nmsm * p.W;
     p.half = 1 << (p.c - 1);
+    // segments grouped by MSM (msm indices non-decreasing): MSM m owns points
+    // [moff[m], moff[m] + mtot[m])
+    uint32_t moff[64] = {0}, mtot[64] = {0};
+    if (nmsm < 1 || nmsm > 64) throw HipError(hipErrorInvalidValue, "nmsm", __FILE__, __LINE__);
+    for (int i = 0; i < nseg; i++) {
+        const uint32_t m = segs[i].msm;
+        if ((int)m >= nmsm || (i && m < segs[i - 1].msm))
+            throw HipError(hipErrorInvalidValue, "segments not grouped by msm", __FILE__, __LINE__);
+        if (!mtot[m]) moff[m] = T.gofs[i];
+        mtot[m] += segs[i].count;
+    }
     for (int i = 0; i < nseg; i++) {
         T.scal[i] = AS_CSC(segs[i].scal);
         T.base[i] = segs[i].base;
-        T.row0[i] = segs[i].msm * p.W;
+        T.row0[i] = segs[i].msm;
         T.wstride[i] = segs[i].wstride;
+        T.moff[i] = moff[segs[i].msm];
+        T.mtot[i] = mtot[segs[i].msm];
     }
     p.E0 = (uint64_t)p.Wd * total;
     p.T = RBK_T;
-    uint64_t D = (uint64_t)p.rows * p.half;
-    uint32_t invalid = (uint32_t)D;
-    p.key_bits = 1;
-    while ((1ULL << p.key_bits) <= D) p.key_bits++;
+    // keys: row << c | slot (slot <= half, half = trash); padding key = rows << c
+    const uint64_t D = (uint64_t)p.rows * p.half;
+    const uint32_t invalid = (uint32_t)p.rows << p.c;
+    p.key_bits = (uint32_t)p.c;   // the sort orders slots within rows
     // slots after pass 1: two per thread chunk, padded to whole blocks
     p.capE = 2 * ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
     p.seglen = p.half < 8 ? p.half : 8;
@@ -787,14 +837,40 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         return p;
     }
     reserve(p);
+    // sort tiles: each row's contiguous entries cut into tiles of at most `tile`
+    uint64_t tile = (p.E0 + 2047) / 2048;
+    tile = std::max<uint64_t>(RS_ITER, (tile + RS_ITER - 1) / RS_ITER * RS_ITER);
+    if (!tiles_ev_) {
+        BPG_HIP(hipEventCreateWithFlags(&tiles_ev_, hipEventDisableTiming));
+        BPG_HIP(hipHostMalloc((void **)&tiles_host_, (size_t)5 * RS_MAXTILES * 4, hipHostMallocDefault));
+        tiles_.grow((size_t)5 * RS_MAXTILES * 4);
+    } else {
+        BPG_HIP(hipEventSynchronize(tiles_ev_));   // the previous job's upload has left the staging buffer
+    }
+    uint32_t nt = 0;
+    for (int r = 0; r < p.rows; r++) {
+        const uint32_t m = p.fixed ? (uint32_t)r : (uint32_t)r % nmsm, w = p.fixed ? 0u : (uint32_t)r / nmsm;
+        const uint64_t rs = p.fixed ? (uint64_t)moff[m] * p.Wd : (uint64_t)w * total + moff[m];
+        const uint64_t rn = p.fixed ? (uint64_t)mtot[m] * p.Wd : mtot[m];
+        const uint32_t t0 = nt;
+        for (uint64_t a = 0; a < rn; a += tile) {
+            if (nt >= RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
+            uint32_t *e = tiles_host_ + 5 * nt++;
+            e[0] = (uint32_t)(rs + a); e[1] = (uint32_t)(rs + std::min<uint64_t>(rn, a + tile));
+            e[4] = (uint32_t)rs;
+        }
+        for (uint32_t k = t0; k < nt; k++) { tiles_host_[5 * k + 2] = t0; tiles_host_[5 * k + 3] = nt; }
+    }
+    BPG_HIP(hipMemcpyAsync(tiles_.p, tiles_host_, (size_t)5 * nt * 4, hipMemcpyHostToDevice, st_));
+    BPG_HIP(hipEventRecord(tiles_ev_, st_));
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     uint8_t *bflag = (uint8_t *)bflag_.p;
     ge *buckets = AS_GE(buckets_.p);
     BPG_HIP(hipMemsetAsync(bflag, 0, D, st_));
     hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.Wd,
-                       p.fixed ? 0u : 1u, (uint32_t)p.half, invalid, keys, vals);
+                       (uint32_t)nmsm, p.fixed ? 1u : 0u, (uint32_t)p.half, keys, vals);
     BPG_HIP(hipGetLastError());
-    radix_sort(keys, vals, keys2, vals2, p.E0, (int)p.key_bits, (uint32_t *)sort_tmp_.p, st_);
+    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
     uint64_t E = p.E0;
     const uint32_t *kin = keys;
@@ -812,16 +888,16 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
                      (fmt == MSM_CACHED ? 8.0 : fmt == MSM_AFFINE ? 9.0 : 7.0) * (double)p.E0);
         if (p.passes == 0 && fmt == MSM_NIELS)
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin, T,
-                               E, invalid, kout, pout, buckets, bflag);
+                               E, invalid, p.c, kout, pout, buckets, bflag);
         else if (p.passes == 0 && fmt == MSM_AFFINE)
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_AFFINE>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
-                               T, E, invalid, kout, pout, buckets, bflag);
+                               T, E, invalid, p.c, kout, pout, buckets, bflag);
         else if (p.passes == 0)
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
-                               T, E, invalid, kout, pout, buckets, bflag);
+                               T, E, invalid, p.c, kout, pout, buckets, bflag);
         else
             hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
-                               T, E, invalid, kout, pout, buckets, bflag);
+                               T, E, invalid, p.c, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
         p.passes++;
         E = 2 * (uint64_t)nblocks * RBK_BLOCK;
@@ -832,7 +908,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         kout = a ? (uint32_t *)rk_b_.p : (uint32_t *)rk_a_.p;
         pout = a ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
     }
-    hipLaunchKernelGGL(k_rbk_final, dim3(nblk(E, 64)), dim3(64), 0, st_, kin, pin, E, invalid, buckets, bflag);
+    hipLaunchKernelGGL(k_rbk_final, dim3(nblk(E, 64)), dim3(64), 0, st_, kin, pin, E, invalid, p.c, buckets, bflag);
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
     ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
     hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
@@ -849,13 +925,13 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     while ((uint32_t)p.rows * split < 256 && split < msplit && p.nseg_per_row / (split * 2) >= 64) split *= 2;
     if (split == 1) {
         hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                           (uint32_t)p.nseg_per_row, lgL, 1u, AS_GE(rows_dev_.p));
+                           (uint32_t)p.nseg_per_row, lgL, 1u, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
     } else {
         ge *parts = AS_GE(rows_dev_.p) + p.rows;
         hipLaunchKernelGGL(k_row_reduce, dim3(p.rows * split), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                           (uint32_t)p.nseg_per_row, lgL, split, parts);
+                           (uint32_t)p.nseg_per_row, lgL, split, (uint32_t)nmsm, (uint32_t)p.W, parts);
         hipLaunchKernelGGL(k_row_final, dim3(nblk(p.rows, 64)), dim3(64), 0, st_, (const ge *)parts, (uint32_t)p.rows,
-                           split, AS_GE(rows_dev_.p));
+                           split, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
     }
     BPG_HIP(hipGetLastError());
     BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
@@ -1611,36 +1687,17 @@ void launch_wtab_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t 
 
 // Output lane i < h1 of vector v (0 = G, 1 = H):
 //   out_i = P_i + sum_{t<3} c_t * P_{i + (t+1) h1}
-// with per-lane-range coefficient digits (signed radix 16); no doublings:
-// every nonzero digit is one table read and one 7M madd. The host flattens
-// the nonzero digits of each (vector, range) into an op list read with scalar
-// loads (blocks never straddle a range), and the table entry of op k+1 is in
-// flight while op k's addition runs.
-#define COMB_MAXSEG (2 * COMB_MAXRANGE)
-#define COMB_MAXOPS 192
-struct CombDev {
-    const void *gens[2];
-    const void *tab[2];
-    void *out[2];
-    uint32_t ntab, nseg;
-    uint32_t start[COMB_MAXSEG], end[COMB_MAXSEG], blk0[COMB_MAXSEG + 1], vec[COMB_MAXSEG], nops[COMB_MAXSEG];
-    // op: table row (w * 8 + m - 1, 9 bits) | t << 9 | neg << 11
-    uint16_t ops[COMB_MAXSEG][COMB_MAXOPS];
-};
-DEVI void comb_entry_load(uint4 (&q)[6], const uint4 *tab, uint32_t op, uint32_t ntab, uint32_t h1, uint32_t i) {
-    const uint32_t jj = i + ((op >> 9) & 3) * h1;
-    const uint4 *e = tab + ((size_t)(op & 511) * ntab + jj) * 6;
+// with per-lane-range coefficient digits (signed radix 16, LSB first); no
+// doublings: every nonzero digit is one table read and one 7M madd.
+__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restrict__ Ap) {
+    const CombArgs &A = *Ap;
+    const uint32_t nb = (A.h1 + 63) / 64;
+    const uint32_t v = blockIdx.x >= nb ? 1 : 0;
+    const uint32_t i = (blockIdx.x - v * nb) * 64 + threadIdx.x;
+    if (i >= A.h1) return;
+    uint32_t r = 0;
 #pragma unroll
-    for (int u = 0; u < 6; u++) q[u] = e[u];
-}
-__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombDev *__restrict__ Ap) {
-    const CombDev &A = *Ap;
-    uint32_t b = blockIdx.x, sg = 0;
-    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
-    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
-    if (i >= A.end[sg]) return;
-    const uint32_t v = A.vec[sg], nops = A.nops[sg], ntab = A.ntab, h1 = A.ntab / 3;
-    const uint16_t *ops = A.ops[sg];
+    for (int k = 1; k < COMB_MAXRANGE; k++) if (k < (int)A.nrange && i >= A.rstart[k]) r = k;
     const uint4 *tab = reinterpret_cast<const uint4 *>(A.tab[v]);
     ge acc;
     ge_identity(acc);
@@ -1649,15 +1706,27 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombDev *__restri
         gen_load(p, reinterpret_cast<const gen *>(A.gens[v]) + i);
         ge_madd(acc, acc, p);
     }
-    uint4 q[6];
-    if (nops) comb_entry_load(q, tab, ops[0], ntab, h1, i);
-    for (uint32_t k = 0; k < nops; k++) {
-        const uint32_t op = ops[k];
-        gen p;
-        genp_unpack(p, q);
-        if (k + 1 < nops) comb_entry_load(q, tab, ops[k + 1], ntab, h1, i);
-        gen_cneg(p, (op >> 11) & 1);
-        ge_madd(acc, acc, p);
+    for (int t = 0; t < 3; t++) {
+        const uint32_t jj = i + (uint32_t)t * A.h1;
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(A.dig[v][r][t]);
+        for (int w4 = 0; w4 < 16; w4++) {
+            const uint32_t packed = dw[w4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int d = (int)(int8_t)(packed >> (8 * k));
+                if (d == 0) continue;
+                const int w = 4 * w4 + k;
+                const int m = d < 0 ? -d : d;
+                const uint4 *e = tab + ((size_t)(w * 8 + m - 1) * A.ntab + jj) * 6;
+                uint4 q[6];
+#pragma unroll
+                for (int u = 0; u < 6; u++) q[u] = e[u];
+                gen p;
+                genp_unpack(p, q);
+                gen_cneg(p, d < 0);
+                ge_madd(acc, acc, p);
+            }
+        }
     }
     gec out;
     ge_to_cached(out, acc);
@@ -1665,46 +1734,29 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombDev *__restri
 }
 void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st) {
     if (!args.h1) return;
-    if (args.nrange < 1 || args.nrange > COMB_MAXRANGE) throw HipError(hipErrorInvalidValue, "comb ranges", __FILE__, __LINE__);
     if (!stage.dev) {
-        BPG_HIP(hipMalloc(&stage.dev, sizeof(CombDev)));
-        BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombDev), hipHostMallocDefault));
+        BPG_HIP(hipMalloc(&stage.dev, sizeof(CombArgs)));
+        BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombArgs), hipHostMallocDefault));
         BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
     } else {
         BPG_HIP(hipEventSynchronize(stage.copied));
     }
-    CombDev &D = *reinterpret_cast<CombDev *>(stage.host);
-    for (int v = 0; v < 2; v++) { D.gens[v] = args.gens[v]; D.tab[v] = args.tab[v]; D.out[v] = args.out[v]; }
-    D.ntab = args.ntab;
-    D.nseg = 0;
-    uint32_t blocks = 0;
+    memcpy(stage.host, &args, sizeof(CombArgs));
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombArgs), hipMemcpyHostToDevice, st));
+    BPG_HIP(hipEventRecord(stage.copied, st));
+    const uint32_t nb = (args.h1 + 63) / 64;
+    // reads 4 level-0 points, writes 1 level-2 point per lane, G and H (SURVEY §8d);
+    // one 7M madd per nonzero digit (+ the base term and the cached output)
     double fem = 0;
     for (uint32_t v = 0; v < 2; v++)
         for (uint32_t r = 0; r < args.nrange; r++) {
             const uint32_t lo = args.rstart[r], hi = r + 1 < args.nrange ? args.rstart[r + 1] : args.h1;
-            if (hi <= lo) continue;
-            const uint32_t sg = D.nseg++;
-            D.start[sg] = lo; D.end[sg] = hi; D.vec[sg] = v; D.blk0[sg] = blocks;
-            blocks += nblk(hi - lo, 64);
-            uint32_t n = 0;
-            for (uint32_t t = 0; t < 3; t++)
-                for (uint32_t w = 0; w < 64; w++) {
-                    const int d = args.dig[v][r][t][w];
-                    if (!d) continue;
-                    const uint32_t m = (uint32_t)(d < 0 ? -d : d);
-                    D.ops[sg][n++] = (uint16_t)((w * 8 + m - 1) | (t << 9) | ((d < 0 ? 1u : 0u) << 11));
-                }
-            D.nops[sg] = n;
-            fem += (double)(hi - lo) * (7.0 * (n + 1) + 1.0);
+            uint32_t nz = 0;
+            for (int t = 0; t < 3; t++) for (int w = 0; w < 64; w++) nz += args.dig[v][r][t][w] != 0;
+            fem += (double)(hi - lo) * (7.0 * (nz + 1) + 1.0);
         }
-    D.blk0[D.nseg] = blocks;
-    if (!blocks) return;
-    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombDev), hipMemcpyHostToDevice, st));
-    BPG_HIP(hipEventRecord(stage.copied, st));
-    // reads 4 level-0 points, writes 1 level-2 point per lane, G and H (SURVEY §8d);
-    // one 7M madd per nonzero digit (+ the base term and the cached output)
     ProfScope ps("ipp_comb_fold", 2.0 * args.h1 * (4 * 64 + 64), fem);
-    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const CombDev *>(stage.dev));
+    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, reinterpret_cast<const CombArgs *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }
 
