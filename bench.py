@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 8 x threads)")
+    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 32 x threads)")
     ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (default min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
@@ -120,7 +120,10 @@ def main():
     ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
     threads = a.threads or max(1, min(16, ncpu // max(world, 1) if world > 1 else ncpu))
     threads = min(threads, 64)
-    batch = a.batch or 8 * threads
+    # 32 proofs per host thread per step: the drain at the end of a step (the
+    # last proofs run with fewer streams beside them) stays ~2% of the step
+    # (profiles/r01p_sweep.txt: 51.5 M at 8 per thread, 56.2 M at 24)
+    batch = a.batch or 32 * threads
 
     inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * rank)
     bpg.set_seed(1000 + rank)
@@ -156,6 +159,19 @@ def main():
     dt = time.perf_counter() - t0
     c1 = os.times()
     host_busy = ((c1.user - c0.user) + (c1.system - c0.system)) / dt   # host cores kept busy by this rank
+    if os.environ.get("BENCH_THREAD_CPU"):   # diagnostic: per-thread CPU seconds (utime, stime)
+        rows = []
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                st = open("/proc/self/task/%s/stat" % tid).read().rsplit(")", 1)[1].split()
+                name = open("/proc/self/task/%s/comm" % tid).read().strip()
+                rows.append((int(st[11]) / 100.0, int(st[12]) / 100.0, tid, name))
+            except OSError:
+                pass
+        rows.sort(reverse=True)
+        print("thread cpu (utime s, stime s, tid, comm), wall %.1f s:" % dt, file=sys.stderr)
+        for r in rows[:48]:
+            print("  %.2f %.2f %s %s" % r, file=sys.stderr)
     L.bpg_profile_enable(0)
     if dist is not None:
         dt = D.max_over_ranks(dt)

@@ -41,6 +41,11 @@ struct ProfSink {
     virtual ~ProfSink() {}
 };
 void set_prof_sink(ProfSink *s);   // thread-local
+// Wait for `ev` by polling with short sleeps. hipEventSynchronize busy-waits
+// (even on hipEventBlockingSync events, measured: a host thread per stream at
+// ~100% CPU), and with a 16-core CPU share the spinning threads got the whole
+// process throttled while the GPU idled.
+void event_wait(hipEvent_t ev);
 ProfSink *prof_sink();
 
 // -------------------------------------------------------------- points

@@ -16,6 +16,7 @@
 
 #include "dev_field.h"
 #include "kernels.h"
+#include <time.h>
 
 namespace bpg {
 namespace dev {
@@ -37,6 +38,17 @@ static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t -
 
 static thread_local ProfSink *tl_sink = nullptr;
 void set_prof_sink(ProfSink *s) { tl_sink = s; }
+void event_wait(hipEvent_t ev) {
+    static const long spin_us = [] { const char *e = getenv("BPG_WAIT_SLEEP_US"); return e ? atol(e) : 20L; }();
+    if (spin_us < 0) { BPG_HIP(hipEventSynchronize(ev)); return; }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) BPG_HIP(e);
+        struct timespec ts{0, spin_us * 1000};
+        nanosleep(&ts, nullptr);
+    }
+}
 ProfSink *prof_sink() { return tl_sink; }
 struct ProfScope {   // brackets the launches issued while it lives
     int h = -1;
@@ -845,7 +857,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         BPG_HIP(hipHostMalloc((void **)&tiles_host_, (size_t)5 * RS_MAXTILES * 4, hipHostMallocDefault));
         tiles_.grow((size_t)5 * RS_MAXTILES * 4);
     } else {
-        BPG_HIP(hipEventSynchronize(tiles_ev_));   // the previous job's upload has left the staging buffer
+        event_wait(tiles_ev_);   // the previous job's upload has left the staging buffer
     }
     uint32_t nt = 0;
     for (int r = 0; r < p.rows; r++) {
@@ -1388,7 +1400,7 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
         BPG_HIP(hipHostMalloc(&stage.host, sizeof(FoldArgs), hipHostMallocDefault));
         BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
     } else {
-        BPG_HIP(hipEventSynchronize(stage.copied));   // previous upload has left the host buffer
+        event_wait(stage.copied);   // previous upload has left the host buffer
     }
     FoldArgs &A = *reinterpret_cast<FoldArgs *>(stage.host);
     A = FoldArgs{};
@@ -1568,7 +1580,7 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
         BPG_HIP(hipHostMalloc(&stage.host, sizeof(Fold2Args), hipHostMallocDefault));
         BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
     } else {
-        BPG_HIP(hipEventSynchronize(stage.copied));   // previous upload has left the host buffer
+        event_wait(stage.copied);   // previous upload has left the host buffer
     }
     Fold2Args &A = *reinterpret_cast<Fold2Args *>(stage.host);
     A.in[0] = Gin; A.in[1] = Hin;
@@ -1739,7 +1751,7 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
         BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombArgs), hipHostMallocDefault));
         BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
     } else {
-        BPG_HIP(hipEventSynchronize(stage.copied));
+        event_wait(stage.copied);
     }
     memcpy(stage.host, &args, sizeof(CombArgs));
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombArgs), hipMemcpyHostToDevice, st));

@@ -224,7 +224,7 @@ struct Workspace : dev::ProfSink {
     hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
     void sync() {
         BPG_HIP(hipEventRecord(done_ev, st));
-        BPG_HIP(hipEventSynchronize(done_ev));
+        event_wait(done_ev);
     }
     ~Workspace() {
         if (done_ev) (void)hipEventDestroy(done_ev);
@@ -568,7 +568,7 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         int buf = 0;
         for (uint64_t i0 = 0; i0 < nd; i0 += CH, buf ^= 1) {
             const uint32_t len = (uint32_t)std::min<uint64_t>(CH, nd - i0);
-            BPG_HIP(hipEventSynchronize(ps.ev[buf]));
+            event_wait(ps.ev[buf]);
             uint8_t *stg = ps.host[buf];
             for (uint32_t i = 0; i < len; i++) {
                 for (int k = 0; k < 8; k++) wp[k] = stg + ((size_t)k * CH + i) * 64;
@@ -579,8 +579,8 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
                                        hipMemcpyHostToDevice, ps.st));
             BPG_HIP(hipEventRecord(ps.ev[buf], ps.st));
         }
-        BPG_HIP(hipEventSynchronize(ps.ev[0]));
-        BPG_HIP(hipEventSynchronize(ps.ev[1]));
+        event_wait(ps.ev[0]);
+        event_wait(ps.ev[1]);
     }
     for (int j = 0; j < 5; j++) {
         S.draw64(tp);
