@@ -206,6 +206,18 @@ struct LazyArgs {
 // msm_scal[0..8h) (layout in kernels.hip), c_L -> [8h], c_R -> [8h+1]
 void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
                           ScD *msm_scal, ScD *partial, hipStream_t st);
+// IPP tail (DESIGN.md "IPP tail without folds"): below a few thousand lanes
+// the generators stay at the last materialised level (M points each) with a
+// per-point weight w_j (Montgomery form), so the round-k base i is
+// sum over j = i mod 2h of w_j P_j. The round's L/R job is 4 segments of M
+// scalars over that level: out = [sLG | sLH | sRG | sRH] (a point not in a
+// segment's half gets 0), c_L -> out[4M], c_R -> out[4M + 1].
+void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, uint32_t M,
+                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, hipStream_t st);
+// after round k: w_j *= rho (Montgomery) for the upper half (j mod 2h >= h),
+// rho_b for the lanes whose pair straddles n
+void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t n, ScD rGa, ScD rGb, ScD rHa,
+                             ScD rHb, hipStream_t st);
 // verifier helpers
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
                       ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st);

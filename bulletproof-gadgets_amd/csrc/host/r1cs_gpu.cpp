@@ -213,7 +213,7 @@ struct Workspace : dev::ProfSink {
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
     DBuf wide, sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
-        ynwR, pts, okflag;
+        ynwR, pts, okflag, wG, wH;
     PtD *rows_host = nullptr;        // pinned, 8 x 64 rows
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
@@ -241,7 +241,7 @@ struct Workspace : dev::ProfSink {
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&wide, &sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
-                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag};
+                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag, &wG, &wH};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -800,9 +800,23 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     Scalar rho_p[4];   // pending fold's scalars (G a/b, H a/b)
     bool pend = false;
     int cur = -1;      // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
+    // Tail (DESIGN.md "IPP tail without folds"): once a materialised level is
+    // short, the remaining rounds keep it and weight its points instead of
+    // folding them (each fold there is a latency-bound launch).
+    static const uint32_t tail_len = [] { const char *e = getenv("BPG_IPP_TAIL"); return e ? (uint32_t)atoi(e) : 4096u; }();
+    bool tail = false;
+    uint32_t M = 0;
     uint32_t len = N;
     for (uint32_t k = 0; len != 1; k++) {
         const uint32_t h = len / 2;
+        if (!tail && !pend && cur >= 0 && len <= tail_len && len >= 4) {
+            tail = true;
+            M = len;
+            ws.wG.grow((size_t)M * sizeof(ScD) + 64);
+            ws.wH.grow((size_t)M * sizeof(ScD) + 64);
+            launch_fill_scalars(as<ScD>(ws.wG), mont(Scalar::one()), M, st);
+            launch_fill_scalars(as<ScD>(ws.wH), mont(Scalar::one()), M, st);
+        }
         IppRoundArgs A;
         A.h = h; A.n = n;
         A.lamG1 = mont(lam); A.lamGu = mont(lam * u);
@@ -822,7 +836,16 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         const bool lazy = pend;
         const size_t hh = h;
         const ScD *cLR;   // c_L, c_R on the device
-        if (lazy) {
+        if (tail) {
+            launch_ipp_prep_tail(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, M, as<ScD>(ws.wG),
+                                 as<ScD>(ws.wH), ms, as<ScD>(ws.partial), st);
+            const size_t mm_ = M;
+            MsmSeg sl[6] = {{ms, Gh, M, 0}, {ms + mm_, Hh, M, 0}, {ms + 4 * mm_, Qb, 1, 0},
+                            {ms + 2 * mm_, Gh, M, 1}, {ms + 3 * mm_, Hh, M, 1}, {ms + 4 * mm_ + 1, Qb, 1, 1}};
+            std::copy(sl, sl + 6, seg);
+            nseg = 6;
+            cLR = ms + 4 * mm_;
+        } else if (lazy) {
             const uint32_t h0 = 2 * h;
             LazyArgs Z;
             Z.h0 = h0;
@@ -845,7 +868,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
             for (const MsmSeg &g : sl) if (!(wsr && g.count == 1 && g.base == Qb)) seg[nseg++] = g;
             cLR = ms + 4 * hh;
         }
-        int ph = ws.prof_begin("msm_ipp", ((lazy ? 8.0 : 4.0) * h + 2) * (64 + 32));
+        int ph = ws.prof_begin("msm_ipp", ((tail ? 2.0 * M : lazy ? 8.0 * h : 4.0 * h) + 2) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, mfmt);
         ws.prof_end(ph);
         if (wsr) BPG_HIP(hipMemcpyAsync(ws.small_host + 1020, cLR, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
@@ -870,7 +893,11 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         Scalar yh = sc_pow_u64(y_inv, h);
         Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
         const int nxt = cur == 0 ? 1 : 0;
-        if (lazy) {
+        if (tail) {
+            if (h > 1)
+                launch_ipp_tail_weights(as<ScD>(ws.wG), as<ScD>(ws.wH), M, h, n, mont(rGa), mont(rGb), mont(rHa),
+                                        mont(rHb), st);
+        } else if (lazy) {
             pend = false;
             if (h > 1) {
                 // level k+1 from level k-1: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
