@@ -27,10 +27,14 @@ import sys
 import time
 
 # HIP hardware queues per process (HIP's default is 4): each host consumer
-# thread drives its own stream, and with 4 queues streams share queues and
-# serialise behind each other's kernels (measured: profiles/r01h_sweep.txt).
-# Must be set before the HIP runtime initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# thread drives its own stream; with fewer queues than streams they serialise
+# behind each other's kernels, with more than 16 the chip does worse again
+# (profiles/r01h_sweep.txt, r01t_sweep.txt). The GPU boxes export the default
+# (GPU_MAX_HW_QUEUES=4), so the bench raises it unless it was set to something
+# else; the runtime reads it when HIP initialises, after this line.
+HW_QUEUES = "16"
+if os.environ.get("GPU_MAX_HW_QUEUES", "4") == "4":
+    os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -43,7 +47,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 32 x threads)")
-    ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (default min(16, cpus))")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
+                         "one HIP stream each (default 24 with >= 16 cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
     return ap.parse_args()
@@ -118,7 +124,10 @@ def main():
     import dist as D
     bpg.lib().bpg_set_device(dev)
     ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
-    threads = a.threads or max(1, min(16, ncpu // max(world, 1) if world > 1 else ncpu))
+    # consumers mostly sleep on the device (event polls), so 24 threads keep
+    # ~9 host cores busy: 8 RNG producers + 16 streams
+    per_rank = ncpu // max(world, 1) if world > 1 else ncpu
+    threads = a.threads or max(1, min(24, per_rank * 3 // 2))
     threads = min(threads, 64)
     # 32 proofs per host thread per step: the drain at the end of a step (the
     # last proofs run with fewer streams beside them) stays ~2% of the step

@@ -47,7 +47,7 @@ static int dup_count(const char *tag) {
 }
 #define BPG_DUPN(tag) for (int dup_i_ = 0, dup_n_ = dup_count(tag); dup_i_ < dup_n_; dup_i_++)
 void event_wait(hipEvent_t ev) {
-    static const long spin_us = [] { const char *e = getenv("BPG_WAIT_SLEEP_US"); return e ? atol(e) : 20L; }();
+    static const long spin_us = [] { const char *e = getenv("BPG_WAIT_SLEEP_US"); return e ? atol(e) : 50L; }();
     if (spin_us < 0) { BPG_HIP(hipEventSynchronize(ev)); return; }
     for (;;) {
         const hipError_t e = hipEventQuery(ev);

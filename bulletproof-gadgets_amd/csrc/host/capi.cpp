@@ -299,9 +299,11 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
         if (threads == 0) threads = 1;
         uint32_t groups = (count + 7) / 8;
-        // producers: ~half the threads (one lockstep group of 8 each); slots
+        // producers: a third of the threads, at most 8 (one lockstep group of 8 each); slots
         // (device buffers) for the groups being drawn plus a queue per consumer
-        uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(groups, threads / 2));
+        // (a producer draws ~20 proofs/s; consumers mostly wait on the device,
+        // so they are the larger share: 24 threads -> 8 producers, 16 consumers)
+        uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(groups, 8u), threads / 3));
         if (const char *e = getenv("BPG_PRODUCERS")) {   // tuning override
             int v = atoi(e);
             if (v >= 1 && (uint32_t)v < threads) P = std::min<uint32_t>(groups, (uint32_t)v);
