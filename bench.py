@@ -51,6 +51,9 @@ def parse():
                     help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
                          "one HIP stream each (default 24 with >= 16 cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("prove", "verify"), default="prove",
+                    help="verify: Verifier::verify throughput over a batch of proofs made before timing "
+                         "(config 5's batch verification; a secondary line, not the headline metric)")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
     return ap.parse_args()
 
@@ -147,6 +150,8 @@ def main():
     def entropies(step):
         return [((rank << 40) | (step << 20) | k).to_bytes(32, "little") for k in range(batch)]
 
+    if a.mode == "verify":
+        return bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropies, q, n, N, W)
     for s in range(a.warmup):
         prep.prove_batch(b"bench", entropies(1000 + s), threads)
     L = bpg.lib()
@@ -253,6 +258,65 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(bpg, a.cpu_leaves)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropies, q, n, N, W):
+    """Verifier::verify (verify.rs:71) throughput: every rank verifies its own
+    batch of proofs (made before timing) with `threads` host threads, one HIP
+    stream each; a step = one pass over the batch. value = proofs verified
+    on all ranks x q / max-over-ranks wall time."""
+    import torch
+    import time as _t
+    batch = a.batch or 8 * threads
+    proofs = prep.prove_batch(b"bench", entropies(777), threads)[:batch]
+    while len(proofs) < batch:
+        proofs += proofs[:batch - len(proofs)]
+    V = _commitments(ctx, syn)
+    prep = ctx.prepare(syn.view, verifier=True)
+    for _ in range(a.warmup):
+        if not all(prep.verify_batch(b"bench", V, proofs, threads)):
+            raise SystemExit("bench: a valid proof was rejected")
+    bad = bytearray(proofs[0])
+    bad[-40] ^= 1
+    if prep.verify_batch(b"bench", V, [bytes(bad)], 1)[0]:
+        raise SystemExit("bench: a tampered proof was accepted")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = _t.perf_counter()
+    ok = True
+    for _ in range(a.steps):
+        ok &= all(prep.verify_batch(b"bench", V, proofs, threads))
+    barrier()
+    dt = _t.perf_counter() - t0
+    if not ok:
+        raise SystemExit("bench: a valid proof was rejected in the timed region")
+    if dist is not None:
+        dt = D.max_over_ranks(dt)
+    t1 = _t.perf_counter()
+    prep.verify_batch(b"bench", V, proofs[:1], 1)
+    single_ms = (_t.perf_counter() - t1) * 1e3
+    total = a.steps * batch * world
+    out = {
+        "metric": "R1CS verify constraints/sec (Ristretto MSM) at %d MI355X" % world,
+        "value": round(total * q / dt, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32 (255-bit integer field/scalar arithmetic)",
+        "data": "synthetic: seeded config-%d statement; proofs made before timing" % a.config,
+        "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
+                   "proofs_per_step_per_gpu": batch, "host_threads_per_gpu": threads,
+                   "parallelism": "independent verifications per GPU (%d ranks)" % world},
+        "proofs_per_s": round(total / dt, 2),
+        "latency_ms_single_verify": round(single_ms, 2),
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

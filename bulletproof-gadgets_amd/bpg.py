@@ -27,6 +27,7 @@ EXPORTS = [
     "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
     "bpg_rng_rate", "bpg_set_fold_tables", "bpg_r1cs_verify_shard", "bpg_point_sum",
     "bpg_kernel_femul", "bpg_set_fold_pairs", "bpg_set_msm_affine", "bpg_set_msm_fixed",
+    "bpg_verify_batch", "bpg_prepare_verifier",
 ]
 
 
@@ -83,7 +84,11 @@ def lib():
         L.bpg_prepare.restype = vp
         L.bpg_prepare.argtypes = [vp, vp]
         L.bpg_prepared_free.argtypes = [vp]
+        L.bpg_prepare_verifier.restype = vp
+        L.bpg_prepare_verifier.argtypes = [vp, vp]
         L.bpg_prove_batch.argtypes = [vp, vp, sz, vp, u32, u32, vp, sz, ctypes.POINTER(sz)]
+        L.bpg_verify_batch.argtypes = [vp, vp, sz, vp, vp, sz, ctypes.POINTER(sz), u32, u32, vp,
+                                       ctypes.POINTER(ctypes.c_int)]
         L.bpg_last_timings.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_msm.argtypes = [vp, vp, vp, u32, vp]
         L.bpg_synthesize.restype = vp
@@ -234,8 +239,11 @@ class Context:
             raise BpgError(last_error())
         return rc == 1, part.raw
 
-    def prepare(self, view):
-        p = lib().bpg_prepare(self.h, ctypes.addressof(view))
+    def prepare(self, view, verifier=False):
+        """HBM-resident circuit: for prove_batch, or with verifier=True for
+        verify_batch (bpg_prepare_verifier)."""
+        f = lib().bpg_prepare_verifier if verifier else lib().bpg_prepare
+        p = f(self.h, ctypes.addressof(view))
         if not p:
             raise BpgError(last_error())
         return Prepared(p)
@@ -260,6 +268,22 @@ class Prepared:
         if rc != 0:
             raise BpgError(last_error())
         return [out.raw[stride * k:stride * k + lens[k]] for k in range(count)]
+
+    def verify_batch(self, label, V, proofs, threads, entropy=b"\x05" * 32):
+        """Verifier::verify over every proof of `proofs` (bytes each) against
+        the compressed commitments V (list of 32-byte points, or their
+        concatenation); list of bools."""
+        if isinstance(V, (list, tuple)):
+            V = b"".join(V)
+        count = len(proofs)
+        stride = max([len(p) for p in proofs] + [1])
+        buf = b"".join(p.ljust(stride, b"\0") for p in proofs)
+        lens = (ctypes.c_size_t * max(count, 1))(*[len(p) for p in proofs])
+        res = (ctypes.c_int * max(count, 1))()
+        rc = lib().bpg_verify_batch(self.h, label, len(label), V, buf, stride, lens, count, threads, entropy, res)
+        if rc != 0:
+            raise BpgError(last_error())
+        return [res[k] == 1 for k in range(count)]
 
     def __del__(self):
         try:

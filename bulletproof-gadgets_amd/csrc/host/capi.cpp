@@ -233,6 +233,11 @@ bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
         return b;
     }, (bpg_prepared *)nullptr);
 }
+bpg_prepared *bpg_prepare_verifier(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
+    bpg_r1cs_view v = *cs;
+    v.a_L = v.a_R = v.a_O = v.v = v.v_blinding = nullptr;
+    return bpg_prepare(ctx, &v);
+}
 void bpg_prepared_free(bpg_prepared *p) { delete p; }
 
 // Persistent host worker pool: each worker owns its thread-local device
@@ -383,6 +388,48 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                 fail(std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr);
             } catch (const std::exception &e) {
                 fail(e.what());
+            }
+        });
+        if (!err.empty()) throw std::runtime_error(err);
+        return 0;
+    }, -1);
+}
+
+// Verifier::verify (verify.rs:71) over `count` proofs of one prepared
+// circuit: each worker thread verifies whole proofs on its own HIP stream
+// (proofs are independent; the sharded single-proof path is
+// bpg_r1cs_verify_shard). results[k] = 1 accept, 0 reject.
+int bpg_verify_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, const uint8_t *V,
+                     const uint8_t *proofs, size_t proof_stride, const size_t *lens, uint32_t count,
+                     uint32_t threads, const uint8_t entropy[32], int *results) {
+    return guarded([&]() -> int {
+        if (!count) return 0;
+        const PreparedCS &cs = *p->p;
+        // the prover's layout drops the constant column the verifier needs
+        if (cs.prover) throw std::runtime_error("circuit prepared for proving: use bpg_prepare_verifier");
+        if (threads == 0) threads = 1;
+        threads = std::min<uint32_t>(threads, count);
+        std::atomic<uint32_t> next(0);
+        std::mutex mu;
+        std::string err;
+        pool().run((int)threads, [&](int) {
+            try {
+                for (;;) {
+                    const uint32_t k = next.fetch_add(1);
+                    if (k >= count) break;
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        if (!err.empty()) break;
+                    }
+                    results[k] = gpu_verify(cs, label, label_len, V, proofs + proof_stride * (size_t)k, lens[k],
+                                            entropy);
+                }
+            } catch (const dev::HipError &e) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (err.empty()) err = std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr;
+            } catch (const std::exception &e) {
+                std::lock_guard<std::mutex> lk(mu);
+                if (err.empty()) err = e.what();
             }
         });
         if (!err.empty()) throw std::runtime_error(err);

@@ -203,6 +203,10 @@ int bpg_point_sum(const uint8_t *points, uint32_t count, uint8_t out[32]);
 typedef struct bpg_prepared bpg_prepared;
 bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs);
 void bpg_prepared_free(bpg_prepared *p);
+/* The same for verification only (witness fields of `cs` ignored): the
+ * handle bpg_verify_batch takes (the prover's layout omits the constant
+ * column, Variable::One, that Verifier::verify flattens). */
+bpg_prepared *bpg_prepare_verifier(bpg_ctx *ctx, const bpg_r1cs_view *cs);
 
 /* Prove `count` independent proofs of one prepared circuit (proof k uses
  * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
@@ -210,6 +214,16 @@ void bpg_prepared_free(bpg_prepared *p);
 int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len,
                     const uint8_t *entropy, uint32_t count, uint32_t threads,
                     uint8_t *proof_out, size_t proof_stride, size_t *lens);
+
+/* Verifier::verify (src/verify.rs:71) over `count` proofs of one circuit
+ * prepared by bpg_prepare_verifier with `threads` host threads, each on its own HIP stream (config 5's
+ * batch verification; independent proofs, so no cross-GPU exchange). Proof k
+ * is proofs + k*proof_stride, lens[k] bytes; V holds the m compressed
+ * commitments. results[k] = 1 accept, 0 reject. Returns 0, or < 0 on error. */
+int bpg_verify_batch(bpg_prepared *p, const uint8_t *label, size_t label_len,
+                     const uint8_t *V, const uint8_t *proofs, size_t proof_stride,
+                     const size_t *lens, uint32_t count, uint32_t threads,
+                     const uint8_t entropy[32], int *results);
 
 /* Per-phase wall-clock timers of the last prove on this thread (ms):
  * [0] transcript+rng, [1] commit MSMs, [2] vectors, [3] IPP, [4] total. */

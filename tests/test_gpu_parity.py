@@ -187,3 +187,29 @@ def test_prepared_batch_matches_single(bpg, ctx, resources):
         single, _ = ctx.r1cs_prove(b"batch", syn.view, ents[k])
         assert p == single
     assert len(set(proofs)) == 6
+
+
+def test_verify_batch(bpg, ctx, resources):
+    """bpg_verify_batch (config 5's batch verification): every valid proof of
+    a batch accepted, each tampered one rejected, same verdicts as the single
+    verifier, whatever the thread count."""
+    fx = read_fixture(os.path.join(resources, "or5"))
+    bpg.set_seed(3)
+    syn = bpg.Synth(fx["inst"], fx["wtns"], fx["gadgets"])
+    prep = ctx.prepare(syn.view)
+    proofs = prep.prove_batch(b"vb", [bytes([k + 1]) * 32 for k in range(6)], threads=2)
+    V = ctx.pedersen(syn.vec("v", syn.m), syn.vec("v_blinding", syn.m))
+    bad = []
+    for k, p in enumerate(proofs[:3]):
+        b = bytearray(p)
+        b[[1, 300, len(b) - 1][k]] ^= 4     # A_I1 point, t_x_blinding, IPP b scalar
+        bad.append(bytes(b))
+    batch = proofs + bad + [proofs[0][:-32]]
+    want = [True] * 6 + [False] * 4
+    vprep = ctx.prepare(syn.view, verifier=True)
+    for threads in (1, 4):
+        assert vprep.verify_batch(b"vb", V, batch, threads) == want
+    assert [ctx.r1cs_verify(b"vb", syn.view, V, p) for p in batch] == want
+    assert vprep.verify_batch(b"other label", V, proofs[:2], 2) == [False, False]
+    with pytest.raises(bpg.BpgError):
+        prep.verify_batch(b"vb", V, proofs[:1], 1)   # prover layout
