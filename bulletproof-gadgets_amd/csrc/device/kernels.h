@@ -169,7 +169,10 @@ void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStr
 // Kernel-argument block staged through pinned host memory to a device buffer
 // (one per stream; the host side is rewritten only after the stream has
 // passed the previous use).
-struct ArgStage { void *dev = nullptr, *host = nullptr; hipEvent_t copied = nullptr; };
+struct ArgStage {
+    void *dev = nullptr, *host = nullptr; hipEvent_t copied = nullptr;
+    void *aux = nullptr; size_t aux_bytes = 0;   // per-stream kernel scratch (fold2 tables), grow-only
+};
 // Gin/Hin: NielsD (in_fmt = MSM_NIELS, the generators) or PtD (MSM_CACHED)
 void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32_t h, uint32_t n, ScD rhoG_a,
                             ScD rhoG_b, ScD rhoH_a, ScD rhoH_b, PtD *Gout, PtD *Hout, ArgStage &stage,

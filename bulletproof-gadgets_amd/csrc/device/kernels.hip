@@ -1477,12 +1477,20 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
 struct Fold2Args {
     const void *in[2];
     gec *out[2];
+    uint32_t *tab;   // k_ipp_fold2g: per-block odd-multiple tables, [block][entry][word][lane]
     uint32_t h1, nseg;
     uint32_t start[FOLD2_MAXSEG], end[FOLD2_MAXSEG], blk0[FOLD2_MAXSEG + 1], vec[FOLD2_MAXSEG];
     uint32_t nops[FOLD2_MAXSEG], tail[FOLD2_MAXSEG];
     // op: gap (doublings before it, 8 bits) | t << 8 (point 0..2) | (m >> 1) << 10 (odd multiple m) | neg << 15
     uint16_t ops[FOLD2_MAXSEG][FOLD2_MAXOPS];
 };
+// op k of a segment's list, read as a 32-bit word: the index is uniform, so
+// this is a scalar load (a 16-bit read is a vector load plus a full vmcnt
+// wait per op)
+DEVI uint32_t fold2_op(const uint16_t *ops, uint32_t k) {
+    const uint32_t w = reinterpret_cast<const uint32_t *>(ops)[k >> 1];
+    return (k & 1) ? w >> 16 : w & 0xffffu;
+}
 // LSB-first width-w NAF of a canonical scalar; returns the digit count
 static int wnaf_digits(const ScD &k, int w, int8_t d[264]) {
     uint32_t x[9];
@@ -1558,14 +1566,31 @@ __global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Ar
     }
     ge acc;
     {
-        const uint32_t op = ops[0];
+        const uint32_t op = fold2_op(ops, 0);
         gec c;
         fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31);
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
+#ifdef BPG_FOLD2_PREFETCH
+    // the next op's multiple is read (from scratch) before this op's doublings
+    gec c;
+    if (nops > 1) { const uint32_t op = fold2_op(ops, 1); fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31); }
     for (uint32_t k = 1; k < nops; k++) {
-        const uint32_t op = ops[k];
+        const uint32_t op = fold2_op(ops, k);
+        const uint32_t g = op & 255;
+        gec cn;
+        if (k + 1 < nops) { const uint32_t on = fold2_op(ops, k + 1); fold2_pick<WN>(cn, tp, (on >> 8) & 3, (on >> 10) & 31); }
+        if (g) {
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+        c = cn;
+    }
+#else
+    for (uint32_t k = 1; k < nops; k++) {
+        const uint32_t op = fold2_op(ops, k);
         const uint32_t g = op & 255;
         if (g) {
             for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
@@ -1574,6 +1599,93 @@ __global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Ar
         gec c;
         fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31);
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+    }
+#endif
+    const uint32_t tail = A.tail[sg];
+    if (tail) {
+        for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
+        ge_dbl_t<true>(acc, acc);
+    }
+    load_as_cached(P0, Pin + i);
+    ge r;
+    ge_add_c(r, acc, P0);
+    gec out;
+    ge_to_cached(out, r);
+    gec_store(A.out[v] + i, out);
+}
+// The WN = 3 fold with the odd-multiple table (P, 3P of the three points,
+// 6 cached points = 960 B per lane) in a global buffer laid out word-major
+// per block ([entry][word][lane]: every load instruction of a wave reads 256
+// contiguous bytes) instead of compiler scratch: the next op's point is
+// loaded before this op's doublings and first used after them, so the load
+// latency hides behind the doubling chain (one wave per SIMD hides nothing
+// else).
+typedef __attribute__((address_space(1))) uint32_t gu32;   // global, not flat: vmcnt only
+DEVI void fold2g_put(uint32_t *tb, const gec &c) {
+    const uint32_t *w = c.YpX.v;
+    gu32 *g = (gu32 *)tb;
+#pragma unroll
+    for (int k = 0; k < 40; k++) g[k * 64] = w[k];
+}
+DEVI void fold2g_get(gec &c, const uint32_t *tb) {
+    uint32_t *w = c.YpX.v;
+    const gu32 *g = (const gu32 *)tb;
+#pragma unroll
+    for (int k = 0; k < 40; k++) w[k] = g[k * 64];
+}
+template <class P>
+__global__ __launch_bounds__(64, 1) void k_ipp_fold2g(const Fold2Args *__restrict__ Ap) {
+    const Fold2Args &A = *Ap;
+    uint32_t b = blockIdx.x, sg = 0;
+    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
+    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
+    if (i >= A.end[sg]) return;
+    const uint32_t v = A.vec[sg], nops = A.nops[sg];
+    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
+    const uint16_t *ops = A.ops[sg];
+    const uint32_t h1 = A.h1;
+    gec P0;
+    if (nops == 0) {
+        load_as_cached(P0, Pin + i);
+        gec_store(A.out[v] + i, P0);
+        return;
+    }
+    uint32_t *tb = A.tab + (size_t)b * (6 * 40 * 64) + threadIdx.x;
+    for (int t = 0; t < 3; t++) {
+        gec c1, c3;
+        load_as_cached(c1, Pin + (size_t)(t + 1) * h1 + i);
+        ge pr, p2, q;
+        fe_sub(pr.X, c1.YpX, c1.YmX);   // projective (2X : 2Y : 2Z), enough to double
+        fe_add(pr.Y, c1.YpX, c1.YmX);
+        pr.Z = c1.Z2;
+        ge_dbl(p2, pr);
+        ge_add_c(q, p2, c1);
+        ge_to_cached(c3, q);
+        fold2g_put(tb + (2 * t) * 40 * 64, c1);
+        fold2g_put(tb + (2 * t + 1) * 40 * 64, c3);
+    }
+    auto entry = [&](uint32_t op) { return tb + (((op >> 8) & 3) * 2 + (((op >> 10) & 31) ? 1 : 0)) * 40 * 64; };
+    ge acc;
+    {
+        const uint32_t op = fold2_op(ops, 0);
+        gec c;
+        fold2g_get(c, entry(op));
+        if (op >> 15) gec_neg(c, c);
+        ge_from_cached(acc, c);
+    }
+    gec c;
+    if (nops > 1) fold2g_get(c, entry(fold2_op(ops, 1)));
+    for (uint32_t k = 1; k < nops; k++) {
+        const uint32_t op = fold2_op(ops, k);
+        const uint32_t g = op & 255;
+        gec cn;
+        if (k + 1 < nops) fold2g_get(cn, entry(fold2_op(ops, k + 1)));
+        if (g) {
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+        c = cn;
     }
     const uint32_t tail = A.tail[sg];
     if (tail) {
@@ -1641,13 +1753,28 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
         }
     A.blk0[A.nseg] = blocks;
     if (!blocks) return;
+    // BPG_FOLD2_GTAB=1: odd-multiple tables in a global buffer (k_ipp_fold2g)
+    static const bool gtab = [] { const char *e = getenv("BPG_FOLD2_GTAB"); return e && atoi(e) == 1; }();
+    const bool use_g = gtab && WN == 3;
+    A.tab = nullptr;
+    if (use_g) {
+        const size_t need = (size_t)blocks * 6 * 40 * 64 * 4;
+        if (stage.aux_bytes < need) {
+            if (stage.aux) BPG_HIP(hipFreeAsync(stage.aux, st));
+            BPG_HIP(hipMallocAsync(&stage.aux, need, st));
+            stage.aux_bytes = need;
+        }
+        A.tab = reinterpret_cast<uint32_t *>(stage.aux);
+    }
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(Fold2Args), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
     // reads 4 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
     ProfScope ps("ipp_fold2", 2.0 * h1 * 5 * 64, fem);
     const Fold2Args *dA = reinterpret_cast<const Fold2Args *>(stage.dev);
     BPG_DUPN("fold2") {
-        if (in_fmt == MSM_NIELS && WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gen, 3>), dim3(blocks), dim3(64), 0, st, dA);
+        if (use_g && in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2g<gen>), dim3(blocks), dim3(64), 0, st, dA);
+        else if (use_g) hipLaunchKernelGGL((k_ipp_fold2g<gec>), dim3(blocks), dim3(64), 0, st, dA);
+        else if (in_fmt == MSM_NIELS && WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gen, 3>), dim3(blocks), dim3(64), 0, st, dA);
         else if (in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2<gen, 2>), dim3(blocks), dim3(64), 0, st, dA);
         else if (WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gec, 3>), dim3(blocks), dim3(64), 0, st, dA);
         else hipLaunchKernelGGL((k_ipp_fold2<gec, 2>), dim3(blocks), dim3(64), 0, st, dA);

@@ -285,6 +285,30 @@ struct Workspace : dev::ProfSink {
     }
 };
 
+// Experiment (BPG_CU_SLICES=k, default off): workspace streams restricted to
+// one of k CU slices (stream i -> slice i mod k), so concurrent proofs stop
+// competing for the same CUs; BPG_CU_SLICE_MODE=0 strided mask bits
+// (j mod k == slice), 1 contiguous ranges.
+static void create_workspace_stream(hipStream_t *st) {
+    static const int slices = [] { const char *e = getenv("BPG_CU_SLICES"); return e ? atoi(e) : 0; }();
+    if (slices < 2) {
+        BPG_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        return;
+    }
+    static std::atomic<int> counter(0);
+    static const int mode = [] { const char *e = getenv("BPG_CU_SLICE_MODE"); return e ? atoi(e) : 0; }();
+    int dev = 0, ncu = 0;
+    BPG_HIP(hipGetDevice(&dev));
+    BPG_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int slice = counter.fetch_add(1) % slices;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int j = 0; j < ncu; j++) {
+        const bool on = mode == 0 ? (j % slices == slice) : (j * slices / ncu == slice);
+        if (on) mask[j / 32] |= 1u << (j % 32);
+    }
+    BPG_HIP(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
+}
+
 Workspace &thread_workspace(int device) {
     static thread_local std::map<int, std::unique_ptr<Workspace>> wss;
     auto &p = wss[device];
@@ -292,7 +316,7 @@ Workspace &thread_workspace(int device) {
         BPG_HIP(hipSetDevice(device));
         p.reset(new Workspace());
         p->device = device;
-        BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+        create_workspace_stream(&p->st);
         BPG_HIP(hipEventCreateWithFlags(&p->done_ev, hipEventBlockingSync | hipEventDisableTiming));
         p->msm.reset(new MsmEngine(p->st));
         BPG_HIP(hipHostMalloc((void **)&p->rows_host, 8 * 64 * sizeof(PtD), hipHostMallocDefault));
