@@ -1572,23 +1572,6 @@ __global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Ar
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
-#ifdef BPG_FOLD2_PREFETCH
-    // the next op's multiple is read (from scratch) before this op's doublings
-    gec c;
-    if (nops > 1) { const uint32_t op = fold2_op(ops, 1); fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31); }
-    for (uint32_t k = 1; k < nops; k++) {
-        const uint32_t op = fold2_op(ops, k);
-        const uint32_t g = op & 255;
-        gec cn;
-        if (k + 1 < nops) { const uint32_t on = fold2_op(ops, k + 1); fold2_pick<WN>(cn, tp, (on >> 8) & 3, (on >> 10) & 31); }
-        if (g) {
-            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
-            ge_dbl_t<true>(acc, acc);
-        }
-        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
-        c = cn;
-    }
-#else
     for (uint32_t k = 1; k < nops; k++) {
         const uint32_t op = fold2_op(ops, k);
         const uint32_t g = op & 255;
@@ -1600,7 +1583,6 @@ __global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Ar
         fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31);
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
     }
-#endif
     const uint32_t tail = A.tail[sg];
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
