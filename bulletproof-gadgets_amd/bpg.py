@@ -14,7 +14,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbpg.so")
+# BPG_LIB_PATH: an in-tree variant build for A/B runs (scripts/ab.sh)
+LIB_PATH = os.environ.get("BPG_LIB_PATH") or os.path.join(HERE, "libbpg.so")
 MAX_PROOF = 417 + 64 * 31
 
 # every symbol include/bpg.h declares

@@ -244,8 +244,12 @@ void launch_to_affine(const NielsD *in, AffD *out, uint32_t count, hipStream_t s
 // buckets + a weighted correction, then a block reduction per row); the host
 // combines rows with c doublings each.
 // ===========================================================================
+#ifndef RBK_T
 #define RBK_T 16
+#endif
+#ifndef RBK_BLOCK
 #define RBK_BLOCK 256
+#endif
 #define RBK_CHUNK (RBK_T * RBK_BLOCK)
 #define MSM_MAXSEG 12
 struct SegTab {
