@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 32 x threads)")
+    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 16 x threads)")
     ap.add_argument("--threads", type=int, default=0,
                     help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
                          "one HIP stream each (default 24 with >= 16 cpus)")
@@ -55,6 +55,8 @@ def parse():
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification; a secondary line, not the headline metric)")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="processes of the all-core CPU leg (default: the host cores this rank may use, at most 16)")
     return ap.parse_args()
 
 
@@ -79,13 +81,14 @@ def pmc_traffic(kernel):
     return None if k is None else k["hbm_bytes_per_launch"]
 
 
-def cpu_baseline(bpg, leaves):
-    """The CPU oracle (oracle/, a C restatement of dalek/bulletproofs with
-    dalek's algorithms, single thread) proving a bounded sample of the same
-    workload family: the config-5 statement with `leaves` Merkle leaves."""
+def _cpu_sample(leaves):
+    """(constraints, seconds) of one warm single-thread oracle proof of the
+    config-5 family with `leaves` Merkle leaves (also run as a child process
+    by the all-core leg: `python bench.py --cpu-sample-child <leaves>`)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import workloads as W
+    bpg = W._bpg()
     inst, wit, gad = W.merkle_set_bound(1005, leaves)
     bpg.set_seed(1)
     syn = bpg.Synth(inst, wit, gad)
@@ -98,17 +101,52 @@ def cpu_baseline(bpg, leaves):
     L.oracle_r1cs_prove(b"bench", 5, view, b"\1" * 32, out, len(out), ctypes.byref(plen), V)
     t0 = time.perf_counter()
     L.oracle_r1cs_prove(b"bench", 5, view, b"\2" * 32, out, len(out), ctypes.byref(plen), V)
-    dt = time.perf_counter() - t0
+    return syn.q, time.perf_counter() - t0, syn.n
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(leaves, procs):
+    """The CPU oracle (oracle/, a C restatement of dalek/bulletproofs with
+    dalek's algorithms; the reference prover is single-threaded) proving a
+    bounded sample of the same workload family: the config-5 statement with
+    `leaves` Merkle leaves. Two legs: one core, and `procs`
+    independent single-thread provers at once (the host's all-core
+    throughput on independent proofs). The full config-5 size on one core is
+    measured once by scripts/cpu_baseline_full.py (profiles/)."""
+    import subprocess
+    q, dt, n = _cpu_sample(leaves)
     N = 1
-    while N < syn.n:
+    while N < n:
         N *= 2
-    return {"value": round(syn.q / dt, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
+    t0 = time.perf_counter()
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-sample-child", str(leaves)],
+                           stdout=subprocess.PIPE, text=True) for _ in range(procs)]
+    res = [json.loads(p.communicate()[0]) for p in ps]
+    wall = time.perf_counter() - t0
+    allcore = sum(r["q"] / r["s"] for r in res)
+    return {"value": round(q / dt, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
             "sample": "oracle/ C restatement (dalek algorithms, 5x51-bit limbs, 1 thread) proving the config-5 "
                       "family with %d Merkle leaves: n=%d, N=2^%d, q=%d, warm generators, %.1f s" %
-                      (leaves, syn.n, N.bit_length() - 1, syn.q, dt)}
+                      (leaves, n, N.bit_length() - 1, q, dt),
+            "all_cores": {"value": round(allcore, 1), "cores": procs, "wall_s": round(wall, 1),
+                          "sample": "%d independent single-thread oracle provers of the same sample at once" % procs},
+            "host": {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": _cpu_model()}}
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-sample-child":
+        q, dt, _ = _cpu_sample(int(sys.argv[2]))
+        print(json.dumps({"q": q, "s": dt}))
+        return
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -132,10 +170,9 @@ def main():
     per_rank = ncpu // max(world, 1) if world > 1 else ncpu
     threads = a.threads or max(1, min(24, per_rank * 3 // 2))
     threads = min(threads, 64)
-    # 32 proofs per host thread per step: the drain at the end of a step (the
-    # last proofs run with fewer streams beside them) stays ~2% of the step
-    # (profiles/r01p_sweep.txt: 51.5 M at 8 per thread, 56.2 M at 24)
-    batch = a.batch or 32 * threads
+    # 16 proofs per host thread per step; the timed steps run as one
+    # continuous pipeline (below), so the end-of-batch drain is paid once
+    batch = a.batch or 16 * threads
 
     inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * rank)
     bpg.set_seed(1000 + rank)
@@ -147,6 +184,7 @@ def main():
     tp = time.perf_counter()
     prep = ctx.prepare(syn.view)
     prepare_ms = (time.perf_counter() - tp) * 1e3
+    setup = ctx.setup_stats()
     q, n = syn.q, syn.n
     N = 1
     while N < n:
@@ -157,8 +195,8 @@ def main():
 
     if a.mode == "verify":
         return bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropies, q, n, N, W)
-    for s in range(a.warmup):
-        prep.prove_batch(b"bench", entropies(1000 + s), threads)
+    if a.warmup:
+        prep.prove_batch(b"bench", sum((entropies(1000 + s) for s in range(a.warmup)), []), threads)
     L = bpg.lib()
     L.bpg_profile_enable(0 if os.environ.get("BENCH_LIVE_TIMING") == "0" else 1)
     L.bpg_kernel_stats_reset()
@@ -171,9 +209,10 @@ def main():
     barrier()
     c0 = os.times()
     t0 = time.perf_counter()
-    proofs = []
-    for s in range(a.steps):
-        proofs.append(prep.prove_batch(b"bench", entropies(s), threads))
+    # the K steps' batches go through the producer/consumer pipeline as one
+    # stream of K x batch independent proofs (a serving prover does not
+    # drain between batches); every proof is one full Prover::prove
+    proofs = prep.prove_batch(b"bench", sum((entropies(s) for s in range(a.steps)), []), threads)
     barrier()
     dt = time.perf_counter() - t0
     c1 = os.times()
@@ -201,7 +240,7 @@ def main():
     single_ms = (time.perf_counter() - t1) * 1e3
     single_phases = bpg.last_timings()
     # a timed proof must verify (device verifier, outside the timed region)
-    sample = proofs[-1][0]
+    sample = proofs[-1]
     ok = ctx.r1cs_verify(b"bench", syn.view, _commitments(ctx, syn), sample)
     if not ok:
         raise SystemExit("bench: a timed proof failed to verify")
@@ -227,7 +266,10 @@ def main():
         sec = ms / lc / 1e3                      # average launch duration
         achieved = (by / lc) / sec / 1e9         # GB/s of algorithmic bytes
         pmc = pmc_traffic(KERNELS[dom])
-        roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm", "achieved": round(achieved, 2),
+        roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm",
+                # the HBM fraction is the metric's; the kernel is limited by its
+                # GF(p) multiply rate and gather latency, see "valu"
+                "limiter": "valu+gather-latency", "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": pmc, "launches": lc, "avg_launch_ms": round(sec * 1e3, 4),
                 "alg_bytes_per_launch": round(by / lc, 1),
@@ -255,15 +297,19 @@ def main():
         "data": "synthetic: seeded config-%d statement (random leaves/witnesses, roots via MiMC)" % a.config,
         "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
                    "proofs_per_step_per_gpu": batch, "host_threads_per_gpu": threads,
-                   "parallelism": "independent proofs per GPU (%d ranks)" % world},
+                   "parallelism": "independent proofs per GPU (%d ranks)" % world,
+                   "pipeline": "the K steps' proofs stream through one producer/consumer pipeline"},
         "host_cores_busy": round(host_busy, 2),
         "latency_ms_single_proof": round(single_ms, 1),
         "cold_setup_ms": round(prepare_ms, 1),
+        "cold_setup_breakdown_ms": {"generators": round(setup["gens_ms"], 1), "comb_tables": round(setup["comb_ms"], 1),
+                                    "generators_from_disk_cache": setup["gens_from_cache"]},
         "phase_ms_single_proof": single_phases,
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(bpg, a.cpu_leaves)
+        aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8
+        out["cpu_baseline"] = cpu_baseline(a.cpu_leaves, a.cpu_procs or max(1, min(16, aff)))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -26,10 +26,15 @@ EXPORTS = [
     "bpg_prove_batch", "bpg_last_timings", "bpg_msm", "bpg_synthesize", "bpg_synthesize_verifier",
     "bpg_synth_view", "bpg_synth_commitments", "bpg_synth_V", "bpg_synth_free", "bpg_mimc_hash",
     "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
-    "bpg_rng_rate", "bpg_set_fold_tables", "bpg_r1cs_verify_shard", "bpg_point_sum",
-    "bpg_kernel_femul", "bpg_set_fold_pairs", "bpg_set_msm_affine", "bpg_set_msm_fixed",
-    "bpg_verify_batch", "bpg_prepare_verifier",
+    "bpg_rng_rate", "bpg_r1cs_verify_shard", "bpg_point_sum", "bpg_kernel_femul",
+    "bpg_verify_batch", "bpg_prepare_verifier", "bpg_gens_cache_dir", "bpg_ctx_set_fold_tables",
+    "bpg_ctx_set_fold_pairs", "bpg_ctx_setup_stats", "bpg_r1cs_prove_sharded", "bpg_cs_create", "bpg_cs_free",
+    "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
+    "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V",
 ]
+
+# bpg_allgather_fn (include/bpg.h)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
 
 class BpgError(RuntimeError):
@@ -39,6 +44,10 @@ class BpgError(RuntimeError):
 class ProofArtifacts(ctypes.Structure):
     _fields_ = [("commitments", ctypes.c_char_p), ("proof", ctypes.POINTER(ctypes.c_uint8)),
                 ("proof_len", ctypes.c_size_t), ("proof_cap", ctypes.c_size_t)]
+
+
+class Lc(ctypes.Structure):
+    _fields_ = [("nterms", ctypes.c_uint32), ("vars", ctypes.c_void_p), ("coeffs", ctypes.c_void_p)]
 
 
 class R1csView(ctypes.Structure):
@@ -78,10 +87,12 @@ def lib():
         L.bpg_r1cs_verify.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp]
         L.bpg_r1cs_verify_shard.argtypes = [vp, vp, sz, vp, vp, vp, sz, vp, u32, u32, vp]
         L.bpg_point_sum.argtypes = [vp, u32, vp]
-        L.bpg_set_fold_tables.argtypes = [ctypes.c_int]
-        L.bpg_set_fold_pairs.argtypes = [ctypes.c_int]
-        L.bpg_set_msm_affine.argtypes = [ctypes.c_int]
-        L.bpg_set_msm_fixed.argtypes = [ctypes.c_int]
+        L.bpg_gens_cache_dir.argtypes = [cp]
+        L.bpg_ctx_set_fold_tables.argtypes = [vp, ctypes.c_int]
+        L.bpg_ctx_set_fold_pairs.argtypes = [vp, ctypes.c_int]
+        L.bpg_ctx_setup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.bpg_r1cs_prove_sharded.argtypes = [vp, vp, sz, vp, vp, u32, u32, ALLGATHER_FN, vp, vp, sz,
+                                             ctypes.POINTER(sz), vp]
         L.bpg_prepare.restype = vp
         L.bpg_prepare.argtypes = [vp, vp]
         L.bpg_prepared_free.argtypes = [vp]
@@ -103,6 +114,23 @@ def lib():
         L.bpg_synth_V.restype = vp
         L.bpg_synth_V.argtypes = [vp]
         L.bpg_synth_free.argtypes = [vp]
+        L.bpg_cs_create.restype = vp
+        L.bpg_cs_create.argtypes = [ctypes.c_int]
+        L.bpg_cs_free.argtypes = [vp]
+        L.bpg_cs_commit.restype = ctypes.c_int64
+        L.bpg_cs_commit.argtypes = [vp, vp, vp]
+        L.bpg_cs_commit_point.restype = ctypes.c_int64
+        L.bpg_cs_commit_point.argtypes = [vp, vp]
+        pl = ctypes.POINTER(Lc)
+        L.bpg_cs_multiply.argtypes = [vp, pl, pl, ctypes.POINTER(u32)]
+        L.bpg_cs_allocate_multiplier.argtypes = [vp, vp, vp, ctypes.POINTER(u32)]
+        L.bpg_cs_constrain.argtypes = [vp, pl]
+        L.bpg_cs_merkle_tree.argtypes = [vp, pl, pl, u32, pl, u32, cp]
+        L.bpg_cs_range_proof.argtypes = [vp, pl, u32, vp]
+        L.bpg_cs_view.restype = ctypes.POINTER(R1csView)
+        L.bpg_cs_view.argtypes = [vp]
+        L.bpg_cs_V.restype = vp
+        L.bpg_cs_V.argtypes = [vp]
         L.bpg_rng_rate.restype = ctypes.c_double
         L.bpg_rng_rate.argtypes = [u32, ctypes.c_int]
         _lib = L
@@ -191,6 +219,105 @@ class Synth:
             pass
 
 
+ONE = 0          # Variable::One() (BPG_VAR(BPG_VAR_ONE, 0))
+ELL = 2**252 + 27742317777372353535851937790883648493
+
+
+def _coeff(c):
+    """A LinearCombination coefficient: kept as given (dalek Scalars from
+    be_to_scalar may be unreduced); negative ints are taken mod l."""
+    if isinstance(c, int):
+        return (c % ELL if c < 0 else c).to_bytes(32, "little")
+    return bytes(c)
+
+
+class GadgetCS:
+    """Gadget-API constraint system (bpg_cs_*): the r1cs::ConstraintSystem
+    calls a Gadget (src/gadget.rs:7-60) makes, recorded like ProverBuffer /
+    VerifierBuffer (src/cs_buffer.rs) and flattened for the inner ABI.
+    A linear combination is a list of (variable, coefficient) pairs, the
+    coefficient an int (< 2^256; negative ints mod l) or 32 LE bytes."""
+
+    def __init__(self, prover=True):
+        self.h = lib().bpg_cs_create(1 if prover else 0)
+        if not self.h:
+            raise BpgError(last_error())
+        self.prover = prover
+        self._m = 0
+
+    @staticmethod
+    def _lc(terms):
+        terms = list(terms)
+        vars_ = (ctypes.c_uint32 * max(len(terms), 1))(*[v for v, _ in terms])
+        co = ctypes.create_string_buffer(b"".join(_coeff(c) for _, c in terms) or b"\0" * 32)
+        lc = Lc(len(terms), ctypes.cast(vars_, ctypes.c_void_p), ctypes.cast(co, ctypes.c_void_p))
+        lc._keep = (vars_, co)
+        return lc
+
+    def commit(self, value, blinding=None):
+        """Prover::commit(v, v_blinding) / Verifier::commit(V) -> Variable."""
+        if self.prover:
+            # v is kept as given (Scalar::from_bits: bit 255 cleared, no reduction)
+            raw = (value & ((1 << 255) - 1)).to_bytes(32, "little") if isinstance(value, int) else bytes(value)
+            r = lib().bpg_cs_commit(self.h, raw, _coeff(blinding))
+        else:
+            r = lib().bpg_cs_commit_point(self.h, value)
+        if r < 0:
+            raise BpgError(last_error())
+        self._m += 1
+        return r
+
+    def multiply(self, left, right):
+        out = (ctypes.c_uint32 * 3)()
+        if lib().bpg_cs_multiply(self.h, ctypes.byref(self._lc(left)), ctypes.byref(self._lc(right)), out) != 0:
+            raise BpgError(last_error())
+        return out[0], out[1], out[2]
+
+    def allocate_multiplier(self, assignment=None):
+        out = (ctypes.c_uint32 * 3)()
+        l, r = (None, None) if assignment is None else (_coeff(assignment[0]), _coeff(assignment[1]))
+        if lib().bpg_cs_allocate_multiplier(self.h, l, r, out) != 0:
+            raise BpgError(last_error())
+        return out[0], out[1], out[2]
+
+    def constrain(self, lc):
+        if lib().bpg_cs_constrain(self.h, ctypes.byref(self._lc(lc))) != 0:
+            raise BpgError(last_error())
+
+    def merkle_tree(self, root, instances, witnesses, pattern):
+        """MerkleTree256::new(root, instance_vars, witness_vars, pattern)
+        .assemble (merkle_tree_gadget.rs:44-56); LCs as above, pattern in the
+        reference's Display form ("H(W W)")."""
+        keep = [self._lc(x) for x in instances], [self._lc(x) for x in witnesses]
+        ia = (Lc * max(len(keep[0]), 1))(*keep[0])
+        wa = (Lc * max(len(keep[1]), 1))(*keep[1])
+        if lib().bpg_cs_merkle_tree(self.h, ctypes.byref(self._lc(root)), ia, len(keep[0]), wa, len(keep[1]),
+                                    _b(pattern)) != 0:
+            raise BpgError(last_error())
+
+    def range_proof(self, x, bits, assignment=None):
+        """utils.rs:5 range_proof(cs, x, n, x_assignment)."""
+        a = None if assignment is None else _coeff(assignment)
+        if lib().bpg_cs_range_proof(self.h, ctypes.byref(self._lc(x)), bits, a) != 0:
+            raise BpgError(last_error())
+
+    @property
+    def view(self):
+        """The flattened system (bpg_r1cs_view; valid until the next call)."""
+        return lib().bpg_cs_view(self.h).contents
+
+    def __del__(self):
+        try:
+            lib().bpg_cs_free(self.h)
+        except Exception:
+            pass
+
+
+def pattern_str(p):
+    """('H', l, r) / ('W',) / ('I',) tuples -> the reference's Display form."""
+    return p[0] if p[0] != "H" else "H(%s %s)" % (pattern_str(p[1]), pattern_str(p[2]))
+
+
 class Context:
     """Device context (generator cache in HBM) for the inner ABI."""
 
@@ -198,6 +325,17 @@ class Context:
         self.h = lib().bpg_ctx_create(device)
         if not self.h:
             raise BpgError(last_error())
+
+    def set_strategy(self, fold_tables=-1, fold_pairs=-1):
+        """IPP fold strategy of this context's calls (bpg_ctx_set_fold_*)."""
+        if lib().bpg_ctx_set_fold_tables(self.h, fold_tables) != 0 or \
+                lib().bpg_ctx_set_fold_pairs(self.h, fold_pairs) != 0:
+            raise BpgError("bad strategy")
+
+    def setup_stats(self):
+        arr = (ctypes.c_double * 3)()
+        lib().bpg_ctx_setup_stats(self.h, arr, 3)
+        return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2])}
 
     def msm(self, scalars, points):
         out = ctypes.create_string_buffer(32)
@@ -221,6 +359,29 @@ class Context:
                                   ctypes.byref(plen), V)
         if rc != 0:
             raise BpgError(last_error())
+        return out.raw[:plen.value], [V.raw[32 * i:32 * i + 32] for i in range(view.m)]
+
+    def r1cs_prove_sharded(self, label, view, entropy, rank, world, allgather):
+        """One proof sharded over `world` ranks (bpg_r1cs_prove_sharded).
+        allgather(payload bytes) -> list of every rank's payload, rank order."""
+        err = []
+
+        def cb(_user, send, nbytes, recv):
+            try:
+                parts = allgather(ctypes.string_at(send, nbytes))
+                ctypes.memmove(recv, b"".join(parts), nbytes * world)
+                return 0
+            except Exception as e:  # the library turns a failed exchange into an error status
+                err.append(e)
+                return -1
+        fn = ALLGATHER_FN(cb)
+        out = ctypes.create_string_buffer(MAX_PROOF)
+        plen = ctypes.c_size_t(0)
+        V = ctypes.create_string_buffer(32 * max(view.m, 1))
+        rc = lib().bpg_r1cs_prove_sharded(self.h, label, len(label), ctypes.addressof(view), entropy, rank, world,
+                                          fn, None, out, MAX_PROOF, ctypes.byref(plen), V)
+        if rc != 0:
+            raise BpgError(last_error() + ("" if not err else " (%r)" % err[0]))
         return out.raw[:plen.value], [V.raw[32 * i:32 * i + 32] for i in range(view.m)]
 
     def r1cs_verify(self, label, view, V, proof, entropy=b"\x05" * 32):

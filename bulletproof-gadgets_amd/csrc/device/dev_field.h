@@ -47,8 +47,6 @@ struct gec { fe YpX, YmX, Z2, T2d; };   // cached: (Y+X, Y-X, 2Z, 2dT)
 // affine Niels (Z = 1): (y+x, y-x, 2dxy), padded to 128 B so a random gather
 // is exactly one 128-B line (generators, decompressed inputs)
 struct gen { fe YpX, YmX, T2d; uint32_t pad[2]; };
-// affine (x, y), Z = 1, canonical, 8 words each: 64 B, half a line per gather
-struct gaf { uint32_t w[16]; };
 
 #define FE_M26 0x3ffffffu
 #define FE_M25 0x1ffffffu
@@ -649,16 +647,6 @@ DEVI void sc_store(sc *dst, const sc &a) {
     d[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
 }
 
-// affine (x, y) -> affine Niels in registers (2M: xy, 2d xy)
-DEVI void gaf_to_niels(gen &q, const gaf &a) {
-    fe x = fe_from_words(a.w[0], a.w[1], a.w[2], a.w[3], a.w[4], a.w[5], a.w[6], a.w[7]);
-    fe y = fe_from_words(a.w[8], a.w[9], a.w[10], a.w[11], a.w[12], a.w[13], a.w[14], a.w[15]);
-    fe t;
-    fe_add_nc(q.YpX, y, x);        // 2T
-    fe_sub_nc(q.YmX, y, x);        // 3T
-    fe_mul(t, x, y);
-    fe_mul(q.T2d, t, FE_D2);
-}
 // Packed affine Niels (comb tables): three canonical field elements as
 // 8 little-endian words each, 96 B = 6 x uint4.
 DEVI void genp_store(uint4 *dst, const gen &q) {

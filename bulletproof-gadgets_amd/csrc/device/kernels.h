@@ -15,8 +15,6 @@ struct ScD { uint32_t v[8]; };
 struct PtD { uint32_t v[40]; };
 // affine Niels (y+x, y-x, 2dxy), Z = 1: 3 x 10 limbs + 2 pad words = 128 B
 struct NielsD { uint32_t v[32]; };
-// affine (x, y), canonical words: 64 B
-struct AffD { uint32_t v[16]; };
 
 #define BPG_HIP(x)                                                                 \
     do {                                                                           \
@@ -60,34 +58,18 @@ void launch_pedersen(const ScD *v, const ScD *vb, uint32_t count, const PtD *tab
 void launch_compress(const PtD *in, uint32_t *out, uint32_t count, hipStream_t st);     // cached in
 void launch_compress(const NielsD *in, uint32_t *out, uint32_t count, hipStream_t st);  // Niels in
 void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count, hipStream_t st);
-void launch_decompress(const uint32_t *in, AffD *out, int *ok, uint32_t count, hipStream_t st);
-// affine copies of Niels points (MSM bases: half the gather bytes)
-void launch_to_affine(const NielsD *in, AffD *out, uint32_t count, hipStream_t st);
 
 // -------------------------------------------------------------- MSM
 #define MSM_CACHED 0   // bases are cached points (PtD)
 #define MSM_NIELS 1    // bases are affine Niels points (NielsD)
-#define MSM_AFFINE 2   // bases are affine (x, y) points (AffD, 64 B)
 struct MsmSeg {
     const ScD *scal;   // canonical scalars (< l)
     const void *base;  // PtD (cached) or NielsD, per the job's format
     uint32_t count;
     uint32_t msm;      // which MSM of the job this segment contributes to
-    // Fixed-base window table: nonzero = window w of point i lives at
-    // base[i + w * wstride] as 2^(WTAB_C w) P_i (all segments of a job or none)
-    uint32_t wstride = 0;
 };
-// Fixed-base window tables of the generators (DESIGN.md "Fixed-base MSMs"):
-// entry [w * N + j] = 2^(16 w) P_j, affine Niels, w < WTAB_W. A job over
-// tables puts all windows of an MSM into one row of 2^15 buckets: no
-// per-window bucket reduction, no host doublings, 16-bit sort keys.
-#define WTAB_C 16
-#define WTAB_W 16
-void launch_wtab_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st);
 struct MsmPlan {
-    int c, W, nmsm, rows, half;   // W: rows per MSM (1 for fixed-base jobs)
-    int Wd;                       // digit windows per scalar
-    bool fixed;
+    int c, W, nmsm, rows, half;   // W: digit windows per scalar = rows per MSM
     uint64_t total;         // points in the job
     uint64_t E0;            // W * total
     uint32_t T;             // chunk size of the reduce-by-key passes
@@ -121,12 +103,14 @@ class MsmEngine {
 };
 
 // -------------------------------------------------------------- scalar vectors
-// out[i] = from_bytes_mod_order_wide(wide[64 i .. 64 i + 64)) (canonical)
-void launch_wide_reduce(const uint8_t *wide, uint32_t count, ScD *out, hipStream_t st);
+// out[j] = from_bytes_mod_order_wide(draw j * stride + offset) (canonical);
+// draw i = wide[64 i .. 64 i + 64)
+void launch_wide_reduce(const uint8_t *wide, uint32_t count, uint32_t stride, uint32_t offset, ScD *out,
+                        hipStream_t st);
 // out[i] = base^(start + i) for i < count, given base2[b] = base^(2^b), b < 32
 void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out, hipStream_t st);
-// out[i] = lo[i & 1023] * hi[i >> 10]
-void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD *out, hipStream_t st);
+// out[i] = lo[i & 1023] * hi[i >> 10] * mult (Montgomery)
+void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD mult, ScD *out, hipStream_t st);
 // flattened_constraints: columns in CSC form; out[col] = sgn * sum coeff * z^(q+1)
 struct CscDev {
     const uint32_t *col_ptr;   // ncol + 1
@@ -171,7 +155,6 @@ void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStr
 // passed the previous use).
 struct ArgStage {
     void *dev = nullptr, *host = nullptr; hipEvent_t copied = nullptr;
-    void *aux = nullptr; size_t aux_bytes = 0;   // per-stream kernel scratch (fold2 tables), grow-only
 };
 // Gin/Hin: NielsD (in_fmt = MSM_NIELS, the generators) or PtD (MSM_CACHED)
 void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32_t h, uint32_t n, ScD rhoG_a,
@@ -225,6 +208,12 @@ void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t 
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
                       ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st);
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st);
+// sharded prover: dst[j] = src[j * stride + offset]
+void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st);
+void launch_gather_niels(const NielsD *src, uint32_t count, uint32_t stride, uint32_t offset, NielsD *dst,
+                         hipStream_t st);
+// Montgomery -> canonical
+void launch_from_mont(const ScD *src, uint32_t count, ScD *dst, hipStream_t st);
 
 }  // namespace dev
 }  // namespace bpg

@@ -38,14 +38,6 @@ static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t -
 
 static thread_local ProfSink *tl_sink = nullptr;
 void set_prof_sink(ProfSink *s) { tl_sink = s; }
-// Perturbation analysis (diagnostic): env BPG_DUP lists kernel tags whose
-// launches are issued twice (all tagged kernels are idempotent), to measure
-// how much each kernel's duration costs the batch throughput.
-static int dup_count(const char *tag) {
-    static const char *list = getenv("BPG_DUP");
-    return list && strstr(list, tag) ? 2 : 1;
-}
-#define BPG_DUPN(tag) for (int dup_i_ = 0, dup_n_ = dup_count(tag); dup_i_ < dup_n_; dup_i_++)
 void event_wait(hipEvent_t ev) {
     static const long spin_us = [] { const char *e = getenv("BPG_WAIT_SLEEP_US"); return e ? atol(e) : 50L; }();
     if (spin_us < 0) { BPG_HIP(hipEventSynchronize(ev)); return; }
@@ -185,49 +177,6 @@ void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count,
     BPG_HIP(hipGetLastError());
 }
 
-DEVI void store_affine(gaf *out, const fe &x, const fe &y) {
-    uint32_t w[16];
-    fe_tow(w, x); fe_tow(w + 8, y);
-    uint4 *d = reinterpret_cast<uint4 *>(out);
-#pragma unroll
-    for (int i = 0; i < 4; i++) d[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-}
-__global__ __launch_bounds__(64) void k_decompress_aff(const uint32_t *__restrict__ in, gaf *__restrict__ out, int *ok,
-                                                        uint32_t count) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    uint32_t w[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = in[8 * (size_t)i + k];
-    ge p;
-    if (!ristretto_decode(p, w)) { ge_identity(p); atomicAnd(ok, 0); }
-    store_affine(out + i, p.X, p.Y);     // decoded points have Z = 1
-}
-void launch_decompress(const uint32_t *in, AffD *out, int *ok, uint32_t count, hipStream_t st) {
-    if (!count) return;
-    hipLaunchKernelGGL(k_decompress_aff, dim3(nblk(count, 64)), dim3(64), 0, st, in, reinterpret_cast<gaf *>(out), ok,
-                       count);
-    BPG_HIP(hipGetLastError());
-}
-// (y+x, y-x) -> (x, y): x = (YpX - YmX) / 2, y = (YpX + YmX) / 2
-__global__ __launch_bounds__(64) void k_to_affine(const gen *__restrict__ in, gaf *__restrict__ out, uint32_t count) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    gen q;
-    gen_load(q, in + i);
-    fe inv2 = fe_from_words(0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
-                            0xffffffffu, 0x3fffffffu);   // (p + 1) / 2
-    fe x, y;
-    fe_sub(x, q.YpX, q.YmX); fe_mul(x, x, inv2);
-    fe_add(y, q.YpX, q.YmX); fe_mul(y, y, inv2);
-    store_affine(out + i, x, y);
-}
-void launch_to_affine(const NielsD *in, AffD *out, uint32_t count, hipStream_t st) {
-    if (!count) return;
-    hipLaunchKernelGGL(k_to_affine, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(in), reinterpret_cast<gaf *>(out),
-                       count);
-    BPG_HIP(hipGetLastError());
-}
 
 // ===========================================================================
 // Pippenger MSM
@@ -257,11 +206,9 @@ struct SegTab {
     const void *base[MSM_MAXSEG];
     uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t row0[MSM_MAXSEG];
-    uint32_t wstride[MSM_MAXSEG];   // fixed-base jobs: points between window tables
-    uint32_t moff[MSM_MAXSEG], mtot[MSM_MAXSEG];   // first point and point count of the segment's MSM
     int n;
 };
-#define MSM_VAL_G 0x00ffffffu       // val = sign << 31 | window << 24 (fixed-base) | point
+#define MSM_VAL_G 0x7fffffffu       // val = sign << 31 | point
 DEVI int seg_of(const SegTab &T, uint32_t g) {
     int si = 0;
 #pragma unroll
@@ -272,10 +219,10 @@ DEVI int seg_of(const SegTab &T, uint32_t g) {
 // Signed c-bit windows. Entry of (point g, window w): key = row << c | slot,
 // slot = |d| - 1 (< half) or half for a zero digit (a trash slot whose run is
 // skipped), val = point | sign << 31. Rows are numbered window-major (row =
-// w * nmsm + msm; fixed-base jobs: row = msm, window in bits 24.. of val), so
+// w * nmsm + msm), so
 // with the entries laid out [w][g] and segments ordered by MSM, the key array
 // is already grouped by row: the sort only orders each row by slot.
-__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t fixed, uint32_t half,
+__global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
@@ -291,8 +238,8 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
         if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
         uint32_t d = (uint32_t)(x >> sh) & mask;
         d += carry;
-        const uint32_t row = fixed ? m : (uint32_t)w * nmsm + m;
-        uint32_t slot = half, val = g | (fixed ? (uint32_t)w << 24 : 0u);
+        const uint32_t row = (uint32_t)w * nmsm + m;
+        uint32_t slot = half, val = g;
         if (d > half) {
             uint32_t mag = full - d;
             carry = 1;
@@ -301,10 +248,8 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
             carry = 0;
             if (d) slot = d - 1;
         }
-        // rows contiguous: [w][g] (one row per window and MSM) or, fixed-base,
-        // [msm][w][g of that MSM]
-        const size_t pos = fixed ? (size_t)T.moff[si] * W + (size_t)w * T.mtot[si] + (g - T.moff[si])
-                                 : (size_t)w * total + g;
+        // rows contiguous: [w][g], one row per window and MSM
+        const size_t pos = (size_t)w * total + g;
         keys[pos] = row << c | slot;
         vals[pos] = val;
     }
@@ -488,21 +433,14 @@ DEVI void rbk_stage(uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t ba
 // (128 B, one line, 7M madd).
 template <int FMT> struct BaseOf { typedef gec T; };
 template <> struct BaseOf<MSM_NIELS> { typedef gen T; };
-template <> struct BaseOf<MSM_AFFINE> { typedef gaf T; };
 template <int FMT>
 DEVI void msm_load_base(typename BaseOf<FMT>::T &p, const SegTab &T, uint32_t v) {
-    const uint32_t g = v & MSM_VAL_G, w = (v >> 24) & 0x7fu;
+    const uint32_t g = v & MSM_VAL_G;
     const int si = seg_of(T, g);
-    pt_load(p, reinterpret_cast<const typename BaseOf<FMT>::T *>(T.base[si]) + (g - T.gofs[si]) +
-                   (size_t)w * T.wstride[si]);
+    pt_load(p, reinterpret_cast<const typename BaseOf<FMT>::T *>(T.base[si]) + (g - T.gofs[si]));
 }
 DEVI void msm_add_loaded(ge &acc, gen &p, bool neg) { gen_cneg(p, neg); ge_madd(acc, acc, p); }
 DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) { gec_cneg(p, neg); ge_add_c(acc, acc, p); }
-DEVI void msm_add_loaded(ge &acc, gaf &p, bool neg) {
-    gen q; gaf_to_niels(q, p);
-    if (neg) { fe t = q.YpX; q.YpX = q.YmX; q.YmX = t; fe_neg(q.T2d, q.T2d); }
-    ge_madd(acc, acc, q);
-}
 
 // FIRST: entries are (key, signed base index) and the gather of entry i+1 is
 // issued before entry i's addition; otherwise entries are slots (key or
@@ -638,39 +576,27 @@ DEVI void ge_dbl_n(ge &r, int n) {
     for (int i = 1; i < n; i++) ge_dbl_t<false>(r, r);
     if (n > 0) ge_dbl_t<true>(r, r);
 }
-// Level 2, ROW_SPLIT blocks per row; block j owns segments [s0, s0 + M)
-// (M = nseg / ROW_SPLIT) and thread t of it [s0 + tK, s0 + tK + K):
-//   sum_{s in block} s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t + s0 * sum_t run_t,
+// Level 2, one block per row; thread t owns segments [tK, tK + K):
+//   sum_s s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t,
 //   sum_t t run_t = sum_{k>=1} suffix_k (suffix scan in LDS).
-// Block j writes P_j = sum A_s + L * (that); k_row_final sums the P_j of a
-// row. L, K and M are powers of two; s0 = j M.
-DEVI void ge_mul_small(ge &r, const ge &p, uint32_t k) {   // k * p, k < 2^8
-    ge acc; ge_identity(acc);
-    for (int b = 7; b >= 0; b--) {
-        ge_dbl(acc, acc);
-        if ((k >> b) & 1) ge_add(acc, acc, p);
-    }
-    r = acc;
-}
+// The row is sum A_s + L * (that). L and K are powers of two.
 // Rows are numbered window-major (row = w * nmsm + msm); results land at
-// msm * W + w, the layout the host combine reads (with split > 1 the block
-// parts stay in row order for k_row_final).
+// msm * W + w, the layout the host combine reads.
 DEVI uint32_t row_perm(uint32_t row, uint32_t nmsm, uint32_t W) { return (row % nmsm) * W + row / nmsm; }
 __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
-                                                    uint32_t nseg, int lgL, uint32_t split, uint32_t nmsm,
-                                                    uint32_t W, ge *__restrict__ parts) {
+                                                    uint32_t nseg, int lgL, uint32_t nmsm, uint32_t W,
+                                                    ge *__restrict__ rows_out) {
     __shared__ ge sh[256];
-    const uint32_t row = blockIdx.x / split, j = blockIdx.x % split, t = threadIdx.x;
-    const uint32_t M = nseg / split, s0 = j * M;
-    const uint32_t K = (M + 255) / 256;
+    const uint32_t row = blockIdx.x, t = threadIdx.x;
+    const uint32_t K = (nseg + 255) / 256;
     int lgK = 0;
     while ((1u << lgK) < K) lgK++;
-    const ge *A = segA + (size_t)row * nseg + s0, *T = segT + (size_t)row * nseg + s0;
+    const ge *A = segA + (size_t)row * nseg, *T = segT + (size_t)row * nseg;
     ge sumA, run, acc, p;
     ge_identity(sumA); ge_identity(run); ge_identity(acc);
     for (int k = (int)K - 1; k >= 0; k--) {
         uint32_t s = t * K + k;
-        if (s >= M) continue;
+        if (s >= nseg) continue;
         ge_load(p, A + s); ge_add(sumA, sumA, p);
         ge_load(p, T + s); ge_add(run, run, p);
         ge_add(acc, acc, run);
@@ -686,21 +612,12 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
         if (act) ge_store(&sh[t], a);
     }
     __syncthreads();
-    ge q, suf, tot;
+    ge q, suf;
     ge_load(suf, &sh[t]);
-    ge_load(tot, &sh[0]);                  // sum of run over the block
     if (t == 0) ge_identity(suf);
     ge_dbl_n(suf, lgK);                    // K * suffix_t
     ge_sub(q, acc, run);
     ge_add(q, q, suf);
-    if (t == 0 && j) {                     // + s0 * sum run, s0 = j * M
-        ge m;
-        int lgM = 0;
-        while ((1u << lgM) < M) lgM++;
-        ge_mul_small(m, tot, j);
-        ge_dbl_n(m, lgM);
-        ge_add(q, q, m);
-    }
     ge_dbl_n(q, lgL);                      // L * (...)
     ge_add(q, q, sumA);
     __syncthreads();
@@ -716,24 +633,14 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
     }
     if (t == 0) {
         ge r; ge_load(r, &sh[0]);
-        ge_store(parts + (split == 1 ? row_perm(blockIdx.x, nmsm, W) : blockIdx.x), r);
+        ge_store(rows_out + row_perm(row, nmsm, W), r);
     }
-}
-__global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ parts, uint32_t rows, uint32_t split,
-                                                  uint32_t nmsm, uint32_t W, ge *__restrict__ rows_out) {
-    const uint32_t row = blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= rows) return;
-    ge acc, p;
-    ge_load(acc, parts + (size_t)row * split);
-    for (uint32_t j = 1; j < split; j++) { ge_load(p, parts + (size_t)row * split + j); ge_add(acc, acc, p); }
-    ge_store(rows_out + row_perm(row, nmsm, W), acc);
 }
 
 static int msm_window(uint64_t total) {
     int lg = 0;
     while ((1ULL << (lg + 1)) <= total) lg++;
-    static const int bias = [] { const char *e = getenv("BPG_MSM_C_BIAS"); return e ? atoi(e) : 3; }();
-    int c = lg - bias;
+    int c = lg - 3;   // lg(points) - 3 (measured best, profiles/r01 MSM window sweeps)
     if (c < 4) c = 4;
     if (c > 16) c = 16;
     return c;
@@ -766,7 +673,7 @@ void MsmEngine::reserve(const MsmPlan &p) {
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
     bflag_.grow((size_t)p.rows * p.half);
     segacc_.grow((size_t)2 * p.rows * p.nseg_per_row * sizeof(ge));
-    rows_dev_.grow((size_t)p.rows * 257 * sizeof(ge));   // rows + per-block parts (split <= 256)
+    rows_dev_.grow((size_t)p.rows * sizeof(ge));
 }
 
 // Sort (keys, vals) by the low key_bits within each row (tiles never straddle
@@ -776,8 +683,7 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
                        uint32_t nt, uint32_t *hist, hipStream_t st) {
     if (!nt || key_bits < 1) return;
     // 8-bit digits only where they save a pass (their scatter costs more LDS)
-    static const bool sort8 = [] { const char *e = getenv("BPG_SORT8"); return !(e && e[0] == '0'); }();
-    const int bits = sort8 && (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
+    const int bits = (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
     for (int shift = 0; shift < key_bits; shift += bits) {
@@ -787,11 +693,9 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
             hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nt, total);
         if (bits == 8)
-            BPG_DUPN("scatter")
             hipLaunchKernelGGL(k_rs_scatter<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist, total,
                                k2, v2);
         else
-            BPG_DUPN("scatter")
             hipLaunchKernelGGL(k_rs_scatter<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist, total,
                                k2, v2);
         std::swap(k, k2);
@@ -802,27 +706,21 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
 
 MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt) {
     if (nseg < 1 || nseg > MSM_MAXSEG) throw HipError(hipErrorInvalidValue, "nseg", __FILE__, __LINE__);
-    if (fmt != MSM_NIELS && fmt != MSM_CACHED && fmt != MSM_AFFINE)
+    if (fmt != MSM_NIELS && fmt != MSM_CACHED)
         throw HipError(hipErrorInvalidValue, "fmt", __FILE__, __LINE__);
     MsmPlan p{};
     SegTab T{};
     uint64_t total = 0;
     T.n = nseg;
-    int nfixed = 0;
     for (int i = 0; i < nseg; i++) {
         T.gofs[i] = (uint32_t)total;
         total += segs[i].count;
-        nfixed += segs[i].wstride ? 1 : 0;
     }
-    if (nfixed && nfixed != nseg) throw HipError(hipErrorInvalidValue, "mixed fixed-base job", __FILE__, __LINE__);
     if (total > MSM_VAL_G) throw HipError(hipErrorInvalidValue, "msm job too large", __FILE__, __LINE__);
     T.gofs[nseg] = (uint32_t)total;
     p.total = total;
-    p.fixed = nfixed > 0;
-    p.c = p.fixed ? WTAB_C : msm_window(total);
-    p.Wd = (254 + p.c - 1) / p.c;
-    if (p.fixed && p.Wd != WTAB_W) throw HipError(hipErrorInvalidValue, "window table", __FILE__, __LINE__);
-    p.W = p.fixed ? 1 : p.Wd;
+    p.c = msm_window(total);
+    p.W = (254 + p.c - 1) / p.c;
     p.nmsm = nmsm;
     p.rows = nmsm * p.W;
     p.half = 1 << (p.c - 1);
@@ -841,11 +739,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         T.scal[i] = AS_CSC(segs[i].scal);
         T.base[i] = segs[i].base;
         T.row0[i] = segs[i].msm;
-        T.wstride[i] = segs[i].wstride;
-        T.moff[i] = moff[segs[i].msm];
-        T.mtot[i] = mtot[segs[i].msm];
     }
-    p.E0 = (uint64_t)p.Wd * total;
+    p.E0 = (uint64_t)p.W * total;
     p.T = RBK_T;
     // keys: row << c | slot (slot <= half, half = trash); padding key = rows << c
     const uint64_t D = (uint64_t)p.rows * p.half;
@@ -875,9 +770,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     }
     uint32_t nt = 0;
     for (int r = 0; r < p.rows; r++) {
-        const uint32_t m = p.fixed ? (uint32_t)r : (uint32_t)r % nmsm, w = p.fixed ? 0u : (uint32_t)r / nmsm;
-        const uint64_t rs = p.fixed ? (uint64_t)moff[m] * p.Wd : (uint64_t)w * total + moff[m];
-        const uint64_t rn = p.fixed ? (uint64_t)mtot[m] * p.Wd : mtot[m];
+        const uint32_t m = (uint32_t)r % nmsm, w = (uint32_t)r / nmsm;
+        const uint64_t rs = (uint64_t)w * total + moff[m];
+        const uint64_t rn = mtot[m];
         const uint32_t t0 = nt;
         for (uint64_t a = 0; a < rn; a += tile) {
             if (nt >= RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
@@ -893,9 +788,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     uint8_t *bflag = (uint8_t *)bflag_.p;
     ge *buckets = AS_GE(buckets_.p);
     BPG_HIP(hipMemsetAsync(bflag, 0, D, st_));
-    BPG_DUPN("digits")
-    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.Wd,
-                       (uint32_t)nmsm, p.fixed ? 1u : 0u, (uint32_t)p.half, keys, vals);
+    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
+                       (uint32_t)nmsm, (uint32_t)p.half, keys, vals);
     BPG_HIP(hipGetLastError());
     radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
@@ -908,25 +802,16 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     for (;;) {
         const uint32_t nblocks = (uint32_t)std::max<uint64_t>(1, (E + RBK_CHUNK - 1) / RBK_CHUNK);
         // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
-        ProfScope ps(p.passes ? nullptr
-                              : (fmt == MSM_CACHED ? "msm_pass1_cached"
-                                                   : fmt == MSM_AFFINE ? "msm_pass1_affine" : "msm_pass1_niels"),
-                     96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels, 9M affine (2M to Niels)
-                     (fmt == MSM_CACHED ? 8.0 : fmt == MSM_AFFINE ? 9.0 : 7.0) * (double)p.E0);
+        ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"),
+                     96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels
+                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);
         if (p.passes == 0 && fmt == MSM_NIELS)
-            BPG_DUPN("rbk1")
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin, T,
                                E, invalid, p.c, kout, pout, buckets, bflag);
-        else if (p.passes == 0 && fmt == MSM_AFFINE)
-            BPG_DUPN("rbk1")
-            hipLaunchKernelGGL((k_rbk_pass<true, MSM_AFFINE>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
-                               T, E, invalid, p.c, kout, pout, buckets, bflag);
         else if (p.passes == 0)
-            BPG_DUPN("rbk1")
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
                                T, E, invalid, p.c, kout, pout, buckets, bflag);
         else
-            BPG_DUPN("rbkN")
             hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
                                T, E, invalid, p.c, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
@@ -942,30 +827,12 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     hipLaunchKernelGGL(k_rbk_final, dim3(nblk(E, 64)), dim3(64), 0, st_, kin, pin, E, invalid, p.c, buckets, bflag);
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
     ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
-    BPG_DUPN("bseg")
     hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
                        (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, segA, segT);
     int lgL = 0;
     while ((1 << lgL) < p.seglen) lgL++;
-    // split rows over several blocks so the level-2 reduction is not a
-    // handful of long serial chains (latency-bound at rows x 256 threads)
-    // (off by default: measured slower with 8 streams sharing the chip, profiles/r01k_ab.txt)
-    static const uint32_t max_split = [] { const char *e = getenv("BPG_ROW_SPLIT"); return e ? (uint32_t)atoi(e) : 1u; }();
-    // (fixed-base jobs have one row per MSM: always split those)
-    const uint32_t msplit = p.fixed ? 64u : max_split;
-    uint32_t split = 1;
-    while ((uint32_t)p.rows * split < 256 && split < msplit && p.nseg_per_row / (split * 2) >= 64) split *= 2;
-    if (split == 1) {
-        BPG_DUPN("rowr")
-        hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                           (uint32_t)p.nseg_per_row, lgL, 1u, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
-    } else {
-        ge *parts = AS_GE(rows_dev_.p) + p.rows;
-        hipLaunchKernelGGL(k_row_reduce, dim3(p.rows * split), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                           (uint32_t)p.nseg_per_row, lgL, split, (uint32_t)nmsm, (uint32_t)p.W, parts);
-        hipLaunchKernelGGL(k_row_final, dim3(nblk(p.rows, 64)), dim3(64), 0, st_, (const ge *)parts, (uint32_t)p.rows,
-                           split, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
-    }
+    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
+                       (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
     BPG_HIP(hipGetLastError());
     BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;
@@ -979,10 +846,13 @@ DEVI sc sc_one_raw() { sc o; sc_zero(o); o.v[0] = 1; return o; }
 
 // Scalar::from_bytes_mod_order_wide of raw 64-byte TranscriptRng draws:
 // lo + hi * 2^256 mod l, with hi * 2^256 = montmul(hi, R^2).
-__global__ void k_wide_reduce(const uint32_t *__restrict__ wide, uint32_t count, sc *__restrict__ out) {
+// Draw j * stride + offset -> out[j] (a rank of the sharded prover reduces
+// only its own lanes).
+__global__ void k_wide_reduce(const uint32_t *__restrict__ wide, uint32_t count, uint32_t stride, uint32_t offset,
+                              sc *__restrict__ out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    const uint4 *w = reinterpret_cast<const uint4 *>(wide + 16 * (size_t)i);
+    const uint4 *w = reinterpret_cast<const uint4 *>(wide + 16 * ((size_t)i * stride + offset));
     uint4 q0 = w[0], q1 = w[1], q2 = w[2], q3 = w[3];
     sc lo, hi, r2, a, b;
     lo.v[0] = q0.x; lo.v[1] = q0.y; lo.v[2] = q0.z; lo.v[3] = q0.w; lo.v[4] = q1.x; lo.v[5] = q1.y; lo.v[6] = q1.z; lo.v[7] = q1.w;
@@ -994,9 +864,11 @@ __global__ void k_wide_reduce(const uint32_t *__restrict__ wide, uint32_t count,
     sc_add(a, a, b);
     sc_store(out + i, a);
 }
-void launch_wide_reduce(const uint8_t *wide, uint32_t count, ScD *out, hipStream_t st) {
+void launch_wide_reduce(const uint8_t *wide, uint32_t count, uint32_t stride, uint32_t offset, ScD *out,
+                        hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_wide_reduce, dim3(nblk(count, 256)), dim3(256), 0, st, (const uint32_t *)wide, count, AS_SC(out));
+    hipLaunchKernelGGL(k_wide_reduce, dim3(nblk(count, 256)), dim3(256), 0, st, (const uint32_t *)wide, count, stride,
+                       offset, AS_SC(out));
     BPG_HIP(hipGetLastError());
 }
 
@@ -1019,17 +891,20 @@ void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out
     hipLaunchKernelGGL(k_pow_table, dim3(nblk(count, 128)), dim3(128), 0, st, AS_CSC(base2), start, count, AS_SC(out));
     BPG_HIP(hipGetLastError());
 }
-__global__ void k_pow_expand(const sc *__restrict__ lo, const sc *__restrict__ hi, uint32_t count, sc *__restrict__ out) {
+__global__ void k_pow_expand(const sc *__restrict__ lo, const sc *__restrict__ hi, uint32_t count, sc mult,
+                             sc *__restrict__ out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     sc a, b, r;
     sc_load(a, lo + (i & 1023)); sc_load(b, hi + (i >> 10));
     mm(r, a, b);
+    mm(r, r, mult);
     sc_store(out + i, r);
 }
-void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD *out, hipStream_t st) {
+void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD mult, ScD *out, hipStream_t st) {
     if (!count) return;
-    hipLaunchKernelGGL(k_pow_expand, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(lo), AS_CSC(hi), count, AS_SC(out));
+    hipLaunchKernelGGL(k_pow_expand, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(lo), AS_CSC(hi), count,
+                       *reinterpret_cast<sc *>(&mult), AS_SC(out));
     BPG_HIP(hipGetLastError());
 }
 
@@ -1481,7 +1356,6 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
 struct Fold2Args {
     const void *in[2];
     gec *out[2];
-    uint32_t *tab;   // k_ipp_fold2g: per-block odd-multiple tables, [block][entry][word][lane]
     uint32_t h1, nseg;
     uint32_t start[FOLD2_MAXSEG], end[FOLD2_MAXSEG], blk0[FOLD2_MAXSEG + 1], vec[FOLD2_MAXSEG];
     uint32_t nops[FOLD2_MAXSEG], tail[FOLD2_MAXSEG];
@@ -1599,92 +1473,6 @@ __global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Ar
     ge_to_cached(out, r);
     gec_store(A.out[v] + i, out);
 }
-// The WN = 3 fold with the odd-multiple table (P, 3P of the three points,
-// 6 cached points = 960 B per lane) in a global buffer laid out word-major
-// per block ([entry][word][lane]: every load instruction of a wave reads 256
-// contiguous bytes) instead of compiler scratch: the next op's point is
-// loaded before this op's doublings and first used after them, so the load
-// latency hides behind the doubling chain (one wave per SIMD hides nothing
-// else).
-typedef __attribute__((address_space(1))) uint32_t gu32;   // global, not flat: vmcnt only
-DEVI void fold2g_put(uint32_t *tb, const gec &c) {
-    const uint32_t *w = c.YpX.v;
-    gu32 *g = (gu32 *)tb;
-#pragma unroll
-    for (int k = 0; k < 40; k++) g[k * 64] = w[k];
-}
-DEVI void fold2g_get(gec &c, const uint32_t *tb) {
-    uint32_t *w = c.YpX.v;
-    const gu32 *g = (const gu32 *)tb;
-#pragma unroll
-    for (int k = 0; k < 40; k++) w[k] = g[k * 64];
-}
-template <class P>
-__global__ __launch_bounds__(64, 1) void k_ipp_fold2g(const Fold2Args *__restrict__ Ap) {
-    const Fold2Args &A = *Ap;
-    uint32_t b = blockIdx.x, sg = 0;
-    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
-    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
-    if (i >= A.end[sg]) return;
-    const uint32_t v = A.vec[sg], nops = A.nops[sg];
-    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
-    const uint16_t *ops = A.ops[sg];
-    const uint32_t h1 = A.h1;
-    gec P0;
-    if (nops == 0) {
-        load_as_cached(P0, Pin + i);
-        gec_store(A.out[v] + i, P0);
-        return;
-    }
-    uint32_t *tb = A.tab + (size_t)b * (6 * 40 * 64) + threadIdx.x;
-    for (int t = 0; t < 3; t++) {
-        gec c1, c3;
-        load_as_cached(c1, Pin + (size_t)(t + 1) * h1 + i);
-        ge pr, p2, q;
-        fe_sub(pr.X, c1.YpX, c1.YmX);   // projective (2X : 2Y : 2Z), enough to double
-        fe_add(pr.Y, c1.YpX, c1.YmX);
-        pr.Z = c1.Z2;
-        ge_dbl(p2, pr);
-        ge_add_c(q, p2, c1);
-        ge_to_cached(c3, q);
-        fold2g_put(tb + (2 * t) * 40 * 64, c1);
-        fold2g_put(tb + (2 * t + 1) * 40 * 64, c3);
-    }
-    auto entry = [&](uint32_t op) { return tb + (((op >> 8) & 3) * 2 + (((op >> 10) & 31) ? 1 : 0)) * 40 * 64; };
-    ge acc;
-    {
-        const uint32_t op = fold2_op(ops, 0);
-        gec c;
-        fold2g_get(c, entry(op));
-        if (op >> 15) gec_neg(c, c);
-        ge_from_cached(acc, c);
-    }
-    gec c;
-    if (nops > 1) fold2g_get(c, entry(fold2_op(ops, 1)));
-    for (uint32_t k = 1; k < nops; k++) {
-        const uint32_t op = fold2_op(ops, k);
-        const uint32_t g = op & 255;
-        gec cn;
-        if (k + 1 < nops) fold2g_get(cn, entry(fold2_op(ops, k + 1)));
-        if (g) {
-            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
-            ge_dbl_t<true>(acc, acc);
-        }
-        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
-        c = cn;
-    }
-    const uint32_t tail = A.tail[sg];
-    if (tail) {
-        for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
-        ge_dbl_t<true>(acc, acc);
-    }
-    load_as_cached(P0, Pin + i);
-    ge r;
-    ge_add_c(r, acc, P0);
-    gec out;
-    ge_to_cached(out, r);
-    gec_store(A.out[v] + i, out);
-}
 void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1, uint32_t nrange,
                       const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][3], PtD *Gout, PtD *Hout,
                       ArgStage &stage, hipStream_t st) {
@@ -1704,7 +1492,7 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
     A.nseg = 0;
     uint32_t blocks = 0;
     double fem = 0;
-    static const int WN = [] { const char *e = getenv("BPG_FOLD2_W"); return (e && atoi(e) == 2) ? 2 : BPG_FOLD2_WNAF; }();
+    constexpr int WN = BPG_FOLD2_WNAF;
     for (uint32_t v = 0; v < 2; v++)
         for (uint32_t r = 0; r < nrange; r++) {
             const uint32_t lo = rstart[r], hi = r + 1 < nrange ? rstart[r + 1] : h1;
@@ -1739,32 +1527,13 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
         }
     A.blk0[A.nseg] = blocks;
     if (!blocks) return;
-    // BPG_FOLD2_GTAB=1: odd-multiple tables in a global buffer (k_ipp_fold2g)
-    static const bool gtab = [] { const char *e = getenv("BPG_FOLD2_GTAB"); return e && atoi(e) == 1; }();
-    const bool use_g = gtab && WN == 3;
-    A.tab = nullptr;
-    if (use_g) {
-        const size_t need = (size_t)blocks * 6 * 40 * 64 * 4;
-        if (stage.aux_bytes < need) {
-            if (stage.aux) BPG_HIP(hipFreeAsync(stage.aux, st));
-            BPG_HIP(hipMallocAsync(&stage.aux, need, st));
-            stage.aux_bytes = need;
-        }
-        A.tab = reinterpret_cast<uint32_t *>(stage.aux);
-    }
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(Fold2Args), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
     // reads 4 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
     ProfScope ps("ipp_fold2", 2.0 * h1 * 5 * 64, fem);
     const Fold2Args *dA = reinterpret_cast<const Fold2Args *>(stage.dev);
-    BPG_DUPN("fold2") {
-        if (use_g && in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2g<gen>), dim3(blocks), dim3(64), 0, st, dA);
-        else if (use_g) hipLaunchKernelGGL((k_ipp_fold2g<gec>), dim3(blocks), dim3(64), 0, st, dA);
-        else if (in_fmt == MSM_NIELS && WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gen, 3>), dim3(blocks), dim3(64), 0, st, dA);
-        else if (in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2<gen, 2>), dim3(blocks), dim3(64), 0, st, dA);
-        else if (WN == 3) hipLaunchKernelGGL((k_ipp_fold2<gec, 3>), dim3(blocks), dim3(64), 0, st, dA);
-        else hipLaunchKernelGGL((k_ipp_fold2<gec, 2>), dim3(blocks), dim3(64), 0, st, dA);
-    }
+    if (in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2<gen, WN>), dim3(blocks), dim3(64), 0, st, dA);
+    else hipLaunchKernelGGL((k_ipp_fold2<gec, WN>), dim3(blocks), dim3(64), 0, st, dA);
     BPG_HIP(hipGetLastError());
 }
 
@@ -1802,30 +1571,6 @@ void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab
     if (!ntab) return;
     hipLaunchKernelGGL(k_comb_build, dim3(nblk(ntab, 64)), dim3(64), 0, st, AS_CGEN(gens), j0, ntab,
                        reinterpret_cast<uint4 *>(tab));
-    BPG_HIP(hipGetLastError());
-}
-
-// Fixed-base window tables: tab[w * N + j] = 2^(16 w) P_j (affine Niels)
-__global__ __launch_bounds__(64) void k_wtab_build(const gen *__restrict__ gens, uint32_t N, gen *__restrict__ tab) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= N) return;
-    gen g;
-    gen_load(g, gens + j);
-    gen_store(tab + j, g);
-    gec c;
-    gen_to_cached(c, g);
-    ge pw;
-    ge_from_cached(pw, c);
-    for (int w = 1; w < WTAB_W; w++) {
-        for (int k = 0; k < WTAB_C - 1; k++) ge_dbl_t<false>(pw, pw);
-        ge_dbl_t<true>(pw, pw);
-        gen e;
-        ge_to_niels(e, pw);
-        gen_store(tab + (size_t)w * N + j, e);
-    }
-}
-void launch_wtab_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st) {
-    hipLaunchKernelGGL(k_wtab_build, dim3(nblk(N, 64)), dim3(64), 0, st, AS_CGEN(gens), N, reinterpret_cast<gen *>(tab));
     BPG_HIP(hipGetLastError());
 }
 
@@ -1900,7 +1645,6 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
             fem += (double)(hi - lo) * (7.0 * (nz + 1) + 1.0);
         }
     ProfScope ps("ipp_comb_fold", 2.0 * args.h1 * (4 * 64 + 64), fem);
-    BPG_DUPN("comb")
     hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, reinterpret_cast<const CombArgs *>(stage.dev));
     BPG_HIP(hipGetLastError());
 }
@@ -2032,6 +1776,50 @@ __global__ void k_fill_scalars(sc *dst, sc val, uint32_t count) {
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st) {
     if (!count) return;
     hipLaunchKernelGGL(k_fill_scalars, dim3(nblk(count, 256)), dim3(256), 0, st, AS_SC(dst), *reinterpret_cast<sc *>(&val), count);
+    BPG_HIP(hipGetLastError());
+}
+// Strided slices for the sharded prover: dst[j] = src[j * stride + offset].
+__global__ void k_gather_scalars(const sc *__restrict__ src, uint32_t count, uint32_t stride, uint32_t offset,
+                                 sc *__restrict__ dst) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count) return;
+    sc a;
+    sc_load(a, src + (size_t)j * stride + offset);
+    sc_store(dst + j, a);
+}
+void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_gather_scalars, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(src), count, stride, offset,
+                       AS_SC(dst));
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_gather_niels(const gen *__restrict__ src, uint32_t count, uint32_t stride, uint32_t offset,
+                               gen *__restrict__ dst) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count) return;
+    gen p;
+    gen_load(p, src + (size_t)j * stride + offset);
+    gen_store(dst + j, p);
+}
+void launch_gather_niels(const NielsD *src, uint32_t count, uint32_t stride, uint32_t offset, NielsD *dst,
+                         hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_gather_niels, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(src), count, stride, offset,
+                       AS_GEN(dst));
+    BPG_HIP(hipGetLastError());
+}
+// Montgomery form -> canonical (MSM scalars from the IPP tail weights)
+__global__ void k_from_mont(const sc *__restrict__ src, uint32_t count, sc *__restrict__ dst) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count) return;
+    sc a, r, one = sc_one_raw();
+    sc_load(a, src + j);
+    mm(r, a, one);
+    sc_store(dst + j, r);
+}
+void launch_from_mont(const ScD *src, uint32_t count, ScD *dst, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_from_mont, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(src), count, AS_SC(dst));
     BPG_HIP(hipGetLastError());
 }
 

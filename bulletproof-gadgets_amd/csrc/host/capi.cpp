@@ -67,26 +67,7 @@ void bpg_set_seed(uint64_t seed) {
     e.cs.seed(seed);
 }
 void bpg_clear_seed(void) { thread_entropy().seeded = false; }
-int bpg_set_fold_tables(int mode) {
-    if (mode < -1 || mode > 1) return -1;
-    set_fold_tables(mode);
-    return 0;
-}
-int bpg_set_fold_pairs(int mode) {
-    if (mode < -1 || mode > 1) return -1;
-    set_fold_pairs(mode);
-    return 0;
-}
-int bpg_set_msm_affine(int mode) {
-    if (mode < -1 || mode > 1) return -1;
-    set_msm_affine(mode);
-    return 0;
-}
-int bpg_set_msm_fixed(int mode) {
-    if (mode < -1 || mode > 1) return -1;
-    set_msm_fixed(mode);
-    return 0;
-}
+void bpg_gens_cache_dir(const char *dir) { set_gens_cache_dir(dir); }
 int bpg_set_device(int device) {
     if (device < 0) return -1;
     g_device = device;
@@ -146,20 +127,41 @@ void free_proof(struct ProofArtifacts *a) {
 }
 
 // ------------------------------------------------------------ inner ABI
-struct bpg_ctx { int device; };
+struct bpg_ctx {
+    int device;
+    Strategy strat;   // IPP fold strategy of the calls made through this handle
+};
 bpg_ctx *bpg_ctx_create(int device) {
     return guarded([&]() -> bpg_ctx * {
         g_device = device;
         require_device();
         DeviceContext::get(device);
-        return new bpg_ctx{device};
+        return new bpg_ctx{device, Strategy()};
     }, (bpg_ctx *)nullptr);
 }
 void bpg_ctx_destroy(bpg_ctx *ctx) { delete ctx; }
+int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) return -1;
+    ctx->strat.fold_tables = mode;
+    return 0;
+}
+int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) return -1;
+    ctx->strat.fold_pairs = mode;
+    return 0;
+}
+int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
+    if (!ctx) return -1;
+    DeviceContext &c = DeviceContext::get(ctx->device);
+    std::lock_guard<std::mutex> lk(c.mu);
+    const double v[3] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0};
+    for (int i = 0; i < n && i < 3; i++) out[i] = v[i];
+    return 0;
+}
 
 int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity) {
     return guarded([&]() -> int {
-        DeviceContext::get(ctx->device).ensure_gens(capacity);
+        DeviceContext::get(ctx->device).gens(capacity);
         return 0;
     }, -1);
 }
@@ -177,8 +179,27 @@ int bpg_r1cs_prove(bpg_ctx *ctx, const uint8_t *label, size_t label_len, const b
                    const uint8_t entropy[32], uint8_t *proof_out, size_t proof_cap, size_t *proof_len, uint8_t *V_out) {
     return guarded([&]() -> int {
         if (!cs->a_L) throw std::runtime_error("prover view without witness");
-        std::unique_ptr<PreparedCS> P = prepare_cs(cs, ctx->device);
+        std::unique_ptr<PreparedCS> P = prepare_cs(cs, ctx->device, ctx->strat);
         std::vector<uint8_t> proof = gpu_prove(*P, label, label_len, entropy);
+        if (proof.size() > proof_cap) throw std::runtime_error("proof buffer too small");
+        memcpy(proof_out, proof.data(), proof.size());
+        *proof_len = proof.size();
+        if (V_out && cs->m) memcpy(V_out, P->V.data(), (size_t)cs->m * 32);
+        return 0;
+    }, -1);
+}
+
+int bpg_r1cs_prove_sharded(bpg_ctx *ctx, const uint8_t *label, size_t label_len, const bpg_r1cs_view *cs,
+                           const uint8_t entropy[32], uint32_t rank, uint32_t world, bpg_allgather_fn allgather,
+                           void *user, uint8_t *proof_out, size_t proof_cap, size_t *proof_len, uint8_t *V_out) {
+    return guarded([&]() -> int {
+        if (!cs->a_L) throw std::runtime_error("prover view without witness");
+        if (!allgather) throw std::runtime_error("NULL all-gather");
+        std::unique_ptr<PreparedCS> P = prepare_cs(cs, ctx->device, ctx->strat, rank, world);
+        AllGather ag = [&](const void *send, size_t bytes, void *recv) {
+            if (allgather(user, send, bytes, recv) != 0) throw std::runtime_error("all-gather failed");
+        };
+        std::vector<uint8_t> proof = gpu_prove(*P, label, label_len, entropy, nullptr, &ag);
         if (proof.size() > proof_cap) throw std::runtime_error("proof buffer too small");
         memcpy(proof_out, proof.data(), proof.size());
         *proof_len = proof.size();
@@ -228,8 +249,8 @@ struct bpg_prepared { std::unique_ptr<PreparedCS> p; };
 bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
     return guarded([&]() -> bpg_prepared * {
         bpg_prepared *b = new bpg_prepared();
-        b->p = prepare_cs(cs, ctx->device);
-        DeviceContext::get(ctx->device).ensure_gens(b->p->N);
+        b->p = prepare_cs(cs, ctx->device, ctx->strat);
+        DeviceContext::get(ctx->device).gens(b->p->N);
         return b;
     }, (bpg_prepared *)nullptr);
 }
@@ -245,6 +266,7 @@ void bpg_prepared_free(bpg_prepared *p) { delete p; }
 namespace {
 struct Pool {
     std::vector<std::thread> workers;
+    std::mutex run_mu;   // one batch at a time: concurrent bpg_*_batch callers queue here
     std::mutex mu;
     std::condition_variable cv, done_cv;
     std::function<void(int)> job;
@@ -273,6 +295,7 @@ struct Pool {
         }
     }
     void run(int n, std::function<void(int)> f) {
+        std::lock_guard<std::mutex> serial(run_mu);
         ensure(n);
         std::unique_lock<std::mutex> lk(mu);
         job = std::move(f);
@@ -333,6 +356,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
             cv.notify_all();
         };
         std::vector<int> slot_of(count, -1);
+        std::vector<ProveTimings> timings(count);
         pool().run((int)(P + C), [&](int id) {
             try {
                 if ((uint32_t)id < P) {
@@ -375,7 +399,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                             k = ready.front();
                             ready.pop_front();
                         }
-                        std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, blocks[k]);
+                        std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, blocks[k], &timings[k]);
                         if (pr.size() > proof_stride) throw std::runtime_error("proof stride too small");
                         memcpy(proof_out + proof_stride * (size_t)k, pr.data(), pr.size());
                         lens[k] = pr.size();
@@ -391,6 +415,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
             }
         });
         if (!err.empty()) throw std::runtime_error(err);
+        last_timings() = timings[count - 1];   // the caller's thread reports the batch's last proof
         return 0;
     }, -1);
 }
@@ -525,6 +550,116 @@ const bpg_r1cs_view *bpg_synth_view(const bpg_synth *s) { return &s->view; }
 const char *bpg_synth_commitments(const bpg_synth *s) { return s->names.c_str(); }
 const uint8_t *bpg_synth_V(const bpg_synth *s) { return s->s.cs->V().data(); }
 void bpg_synth_free(bpg_synth *s) { delete s; }
+
+// Gadget-API recorder (bulletproofs r1cs::ConstraintSystem as the
+// reference's ProverBuffer / VerifierBuffer record it, cs_buffer.rs:22-199).
+struct bpg_cs {
+    ConstraintSystem cs;
+    bpg_r1cs_view view;
+    explicit bpg_cs(bool prover) : cs(prover), view() {}
+};
+static LC to_lc(const bpg_lc *l) {
+    LC r;
+    if (!l) return r;
+    if (l->nterms && (!l->vars || !l->coeffs)) throw std::runtime_error("NULL linear combination");
+    r.t.reserve(l->nterms);
+    for (uint32_t k = 0; k < l->nterms; k++) {   // kept as given, like dalek's (possibly unreduced) Scalars
+        Scalar c;
+        memcpy(c.v, l->coeffs + 32 * (size_t)k, 32);
+        r.t.push_back({l->vars[k], c});
+    }
+    return r;
+}
+static void check_lc_vars(const bpg_cs *c, const LC &lc) {
+    for (auto &t : lc.t) {
+        const uint32_t kind = BPG_VAR_KIND(t.first), idx = BPG_VAR_INDEX(t.first);
+        const bool ok = kind == BPG_VAR_ONE ? idx == 0
+                        : kind == BPG_VAR_V  ? idx < c->cs.m()
+                        : (kind >= BPG_VAR_L && kind <= BPG_VAR_O) ? idx < c->cs.n() : false;
+        if (!ok) throw std::runtime_error("linear combination names an unknown variable");
+    }
+}
+bpg_cs *bpg_cs_create(int prover) {
+    return guarded([&]() -> bpg_cs * { return new bpg_cs(prover != 0); }, (bpg_cs *)nullptr);
+}
+void bpg_cs_free(bpg_cs *c) { delete c; }
+int64_t bpg_cs_commit(bpg_cs *c, const uint8_t v[32], const uint8_t v_blinding[32]) {
+    return guarded([&]() -> int64_t {
+        if (!c->cs.prover()) throw std::runtime_error("verifier-side recorder: use bpg_cs_commit_point");
+        Scalar a, b;
+        memcpy(a.v, v, 32);            // Scalar::from_bits: kept as given (prove.rs commits may be unreduced)
+        memcpy(b.v, v_blinding, 32);
+        return (int64_t)c->cs.commit_value(a, b);
+    }, (int64_t)-1);
+}
+int64_t bpg_cs_commit_point(bpg_cs *c, const uint8_t V[32]) {
+    return guarded([&]() -> int64_t {
+        if (c->cs.prover()) throw std::runtime_error("prover-side recorder: use bpg_cs_commit");
+        return (int64_t)c->cs.commit_point(V);
+    }, (int64_t)-1);
+}
+int bpg_cs_multiply(bpg_cs *c, const bpg_lc *left, const bpg_lc *right, uint32_t out[3]) {
+    return guarded([&]() -> int {
+        LC l = to_lc(left), r = to_lc(right);
+        check_lc_vars(c, l);
+        check_lc_vars(c, r);
+        ConstraintSystem::Triple t = c->cs.multiply(l, r);
+        out[0] = t.l; out[1] = t.r; out[2] = t.o;
+        return 0;
+    }, -1);
+}
+int bpg_cs_allocate_multiplier(bpg_cs *c, const uint8_t *left, const uint8_t *right, uint32_t out[3]) {
+    return guarded([&]() -> int {
+        ConstraintSystem::Triple t;
+        if (c->cs.prover()) {
+            if (!left || !right) throw std::runtime_error("prover-side allocate_multiplier needs an assignment");
+            Scalar l = Scalar::reduce(left), r = Scalar::reduce(right);
+            t = c->cs.allocate_multiplier(&l, &r);
+        } else {
+            t = c->cs.allocate_multiplier(nullptr, nullptr);
+        }
+        out[0] = t.l; out[1] = t.r; out[2] = t.o;
+        return 0;
+    }, -1);
+}
+int bpg_cs_constrain(bpg_cs *c, const bpg_lc *lc) {
+    return guarded([&]() -> int {
+        LC l = to_lc(lc);
+        check_lc_vars(c, l);
+        c->cs.constrain(l);
+        return 0;
+    }, -1);
+}
+int bpg_cs_merkle_tree(bpg_cs *c, const bpg_lc *root, const bpg_lc *inst, uint32_t ninst, const bpg_lc *wit,
+                       uint32_t nwit, const char *pattern) {
+    return guarded([&]() -> int {
+        if (!pattern) throw std::runtime_error("NULL pattern");
+        std::vector<LC> i, w;
+        for (uint32_t k = 0; k < ninst; k++) { i.push_back(to_lc(inst + k)); check_lc_vars(c, i.back()); }
+        for (uint32_t k = 0; k < nwit; k++) { w.push_back(to_lc(wit + k)); check_lc_vars(c, w.back()); }
+        LC r = to_lc(root);
+        check_lc_vars(c, r);
+        merkle_tree_assemble(c->cs, r, std::move(i), std::move(w), pattern);
+        return 0;
+    }, -1);
+}
+int bpg_cs_range_proof(bpg_cs *c, const bpg_lc *x, uint32_t bits, const uint8_t *x_assignment) {
+    return guarded([&]() -> int {
+        if (bits > 256) throw std::runtime_error("range proof wider than 256 bits");
+        LC l = to_lc(x);
+        check_lc_vars(c, l);
+        Scalar a;
+        if (x_assignment) memcpy(a.v, x_assignment, 32);
+        if (c->cs.prover() && !x_assignment) throw std::runtime_error("prover-side range proof needs the assignment");
+        range_proof_assemble(c->cs, l, bits, c->cs.prover() ? &a : nullptr);
+        return 0;
+    }, -1);
+}
+const bpg_r1cs_view *bpg_cs_view(bpg_cs *c) {
+    c->view = c->cs.view(true);
+    return &c->view;
+}
+const uint8_t *bpg_cs_V(const bpg_cs *c) { return c->cs.V().data(); }
 
 int bpg_mimc_hash(const uint8_t *data, size_t len, uint8_t out[32]) {
     return guarded([&]() -> int {

@@ -6,6 +6,7 @@
 #include "r1cs_gpu.h"
 
 #include <stdlib.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -59,124 +60,184 @@ DeviceContext &DeviceContext::get(int device) {
     return *p;
 }
 
-// BulletproofGens::new(N, 1): chains SHAKE256("GeneratorsChain" || tag || u32le(0))
-// squeezed 64 bytes per point on the host (the XOF is one serial chain),
-// Elligator x2 + add on the device.
-void DeviceContext::ensure_gens(uint32_t N) {
-    std::lock_guard<std::mutex> lk(mu);
-    if (N <= gens_cap) return;
-    uint32_t cap = std::max<uint32_t>(N, 64);
-    BPG_HIP(hipSetDevice(device));
-    NielsD *nG = nullptr, *nH = nullptr;
-    BPG_HIP(hipMalloc(&nG, (size_t)cap * sizeof(NielsD)));
-    BPG_HIP(hipMalloc(&nH, (size_t)cap * sizeof(NielsD)));
-    std::vector<uint8_t> uni((size_t)cap * 64);
-    uint8_t *duni = nullptr;
-    BPG_HIP(hipMalloc(&duni, uni.size()));
-    for (int which = 0; which < 2; which++) {
-        uint8_t label[20];
-        memcpy(label, "GeneratorsChain", 15);
-        label[15] = which ? 'H' : 'G';
-        label[16] = label[17] = label[18] = label[19] = 0;
-        Shake256 xof;
-        xof.init_absorb(label, 20);
-        xof.squeeze(uni.data(), uni.size());
-        BPG_HIP(hipMemcpy(duni, uni.data(), uni.size(), hipMemcpyHostToDevice));
-        launch_gens_map(duni, which ? nH : nG, cap, 0);
-    }
-    AffD *aG = nullptr, *aH = nullptr;
-    BPG_HIP(hipMalloc(&aG, (size_t)cap * sizeof(AffD)));
-    BPG_HIP(hipMalloc(&aH, (size_t)cap * sizeof(AffD)));
-    launch_to_affine(nG, aG, cap, 0);
-    launch_to_affine(nH, aH, cap, 0);
-    BPG_HIP(hipDeviceSynchronize());
-    (void)hipFree(duni);
-    if (G) (void)hipFree(G);
-    if (H) (void)hipFree(H);
-    if (Ga) (void)hipFree(Ga);
-    if (Ha) (void)hipFree(Ha);
-    G = nG; H = nH; Ga = aG; Ha = aH; gens_cap = cap;
-}
-
-static std::atomic<int> g_fold_tables(-1);
-void set_fold_tables(int mode) { g_fold_tables = mode; }
-static bool fold_tables_enabled() {
-    int m = g_fold_tables;
-    if (m >= 0) return m != 0;
-    const char *e = getenv("BPG_FOLD_TABLES");
-    return !(e && e[0] == '0');
-}
-static std::atomic<int> g_fold_pairs(-1);
-void set_fold_pairs(int mode) { g_fold_pairs = mode; }
-static bool fold_pairs_enabled() {
-    int m = g_fold_pairs;
-    if (m >= 0) return m != 0;
-    const char *e = getenv("BPG_FOLD_PAIRS");
-    return !(e && e[0] == '0');
-}
-static std::atomic<int> g_msm_affine(-1);
-void set_msm_affine(int mode) { g_msm_affine = mode; }
-static bool msm_affine_enabled() {
-    int m = g_msm_affine;
-    if (m >= 0) return m != 0;
-    const char *e = getenv("BPG_MSM_AFFINE");
-    return e && e[0] == '1';
-}
-static std::atomic<int> g_msm_fixed(-1);
-void set_msm_fixed(int mode) { g_msm_fixed = mode; }
-static bool msm_fixed_enabled() {
-    int m = g_msm_fixed;
-    if (m >= 0) return m != 0;
-    const char *e = getenv("BPG_MSM_FIXED");
-    return e && e[0] == '1';
-}
-WinTables::~WinTables() {
+GenSet::~GenSet() {
     if (G || H) (void)hipSetDevice(device);
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
-}
-std::shared_ptr<WinTables> DeviceContext::ensure_wtab(uint32_t N) {
-    if (N < 2 || !msm_fixed_enabled()) return nullptr;
-    ensure_gens(N);
-    std::lock_guard<std::mutex> lk(mu);
-    if (wtab && wtab->N >= N) return wtab;
-    BPG_HIP(hipSetDevice(device));
-    wtab.reset();
-    const size_t bytes = (size_t)WTAB_W * N * sizeof(NielsD);   // per vector
-    size_t free_b = 0, total_b = 0;
-    BPG_HIP(hipMemGetInfo(&free_b, &total_b));
-    if (2 * bytes + ((size_t)16 << 30) > free_b) return nullptr;
-    std::shared_ptr<WinTables> t(new WinTables());
-    t->device = device;
-    t->N = N;
-    if (hipMalloc((void **)&t->G, bytes) != hipSuccess || hipMalloc((void **)&t->H, bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    launch_wtab_build(G, N, t->G, 0);
-    launch_wtab_build(H, N, t->H, 0);
-    BPG_HIP(hipDeviceSynchronize());
-    wtab = t;
-    return wtab;
 }
 CombTables::~CombTables() {
     if (tabG || tabH) (void)hipSetDevice(device);
     if (tabG) (void)hipFree(tabG);
     if (tabH) (void)hipFree(tabH);
 }
-std::shared_ptr<CombTables> DeviceContext::ensure_comb(uint32_t N) {
-    if (N < 8 || !fold_tables_enabled()) return nullptr;
-    ensure_gens(N);
+static bool env_off(const char *name) {
+    const char *e = getenv(name);
+    return e && e[0] == '0';
+}
+bool Strategy::tables() const { return fold_tables >= 0 ? fold_tables != 0 : !env_off("BPG_FOLD_TABLES"); }
+bool Strategy::pairs() const { return fold_pairs >= 0 ? fold_pairs != 0 : !env_off("BPG_FOLD_PAIRS"); }
+
+static std::mutex g_cache_mu;
+static std::string g_cache_dir;
+static bool g_cache_dir_set = false;
+void set_gens_cache_dir(const char *dir) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_cache_dir = dir ? dir : "";
+    g_cache_dir_set = true;
+}
+static std::string gens_cache_dir() {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    if (g_cache_dir_set) return g_cache_dir;
+    const char *e = getenv("BPG_GENS_CACHE");
+    return e ? e : "";
+}
+
+// The 64-byte uniform strings of generator chain `tag` (G or H):
+// SHAKE256("GeneratorsChain" || tag || u32le(0)) squeezed 64 bytes per point
+// (generators.rs GeneratorsChain; one serial XOF per chain).
+static void gens_uniform(char tag, uint8_t *out, size_t points) {
+    uint8_t label[20];
+    memcpy(label, "GeneratorsChain", 15);
+    label[15] = (uint8_t)tag;
+    label[16] = label[17] = label[18] = label[19] = 0;
+    Shake256 xof;
+    xof.init_absorb(label, 20);
+    xof.squeeze(out, points * 64);
+}
+
+// On-disk cache file of a full set: magic, N, a checksum, then G and H as
+// device affine Niels points. Validated on load by the checksum and by
+// recomputing the first points of both chains on the host (a prefix of the
+// XOF, so the check costs microseconds, not the chain).
+static const uint64_t GENS_MAGIC = 0x32736e6567677062ULL;   // "bpggens2"
+static std::string gens_cache_path(const std::string &dir, uint32_t N) {
+    return dir + "/bpg_gens_" + std::to_string(N) + ".bin";
+}
+static uint64_t gens_checksum(const std::vector<dev::NielsD> &G, const std::vector<dev::NielsD> &H) {
+    uint64_t h = 0x9e3779b97f4a7c15ULL;
+    for (const std::vector<dev::NielsD> *v : {&G, &H}) {
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(v->data());
+        const size_t nw = v->size() * sizeof(dev::NielsD) / 8;
+        for (size_t i = 0; i < nw; i++) h = (h ^ w[i]) * 0x100000001b3ULL + (h >> 29);
+    }
+    return h;
+}
+static bool gens_cache_check(const std::vector<dev::NielsD> &G, const std::vector<dev::NielsD> &H) {
+    const uint32_t K = (uint32_t)std::min<size_t>(4, G.size());
+    uint8_t uni[64 * 4];
+    for (int which = 0; which < 2; which++) {
+        gens_uniform(which ? 'H' : 'G', uni, K);
+        for (uint32_t k = 0; k < K; k++) {
+            Point p;
+            ristretto_from_uniform(p, uni + 64 * k);
+            dev::NielsD want;
+            pt_to_dev_niels(want.v, p);
+            if (memcmp(&want, which ? &H[k] : &G[k], sizeof(want))) return false;
+        }
+    }
+    return true;
+}
+
+std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uint32_t world) {
+    if (world < 1 || rank >= world || N % world) throw std::runtime_error("bad generator slice");
     std::lock_guard<std::mutex> lk(mu);
-    if (comb && comb->N == N) return comb;
+    BPG_HIP(hipSetDevice(device));
+    if (!full || full->N < N) {
+        const double t0 = now_ms();
+        const uint32_t cap = std::max<uint32_t>(N, 64);
+        std::shared_ptr<GenSet> gs(new GenSet());
+        gs->device = device;
+        gs->N = cap;
+        BPG_HIP(hipMalloc(&gs->G, (size_t)cap * sizeof(dev::NielsD)));
+        BPG_HIP(hipMalloc(&gs->H, (size_t)cap * sizeof(dev::NielsD)));
+        const std::string dir = gens_cache_dir();
+        bool loaded = false;
+        if (!dir.empty()) {
+            if (FILE *f = fopen(gens_cache_path(dir, cap).c_str(), "rb")) {
+                uint64_t hdr[3] = {0, 0, 0};
+                std::vector<dev::NielsD> hG(cap), hH(cap);
+                if (fread(hdr, 8, 3, f) == 3 && hdr[0] == GENS_MAGIC && hdr[1] == cap &&
+                    fread(hG.data(), sizeof(dev::NielsD), cap, f) == cap &&
+                    fread(hH.data(), sizeof(dev::NielsD), cap, f) == cap && hdr[2] == gens_checksum(hG, hH) &&
+                    gens_cache_check(hG, hH)) {
+                    BPG_HIP(hipMemcpy(gs->G, hG.data(), (size_t)cap * sizeof(dev::NielsD), hipMemcpyHostToDevice));
+                    BPG_HIP(hipMemcpy(gs->H, hH.data(), (size_t)cap * sizeof(dev::NielsD), hipMemcpyHostToDevice));
+                    loaded = true;
+                }
+                fclose(f);
+            }
+        }
+        if (!loaded) {
+            // host SHAKE chains, Elligator x2 + add on the device
+            std::vector<uint8_t> uni((size_t)cap * 64);
+            uint8_t *duni = nullptr;
+            BPG_HIP(hipMalloc(&duni, uni.size()));
+            for (int which = 0; which < 2; which++) {
+                gens_uniform(which ? 'H' : 'G', uni.data(), cap);
+                BPG_HIP(hipMemcpy(duni, uni.data(), uni.size(), hipMemcpyHostToDevice));
+                launch_gens_map(duni, which ? gs->H : gs->G, cap, 0);
+            }
+            BPG_HIP(hipDeviceSynchronize());
+            (void)hipFree(duni);
+            if (!dir.empty()) {   // write-then-rename: concurrent processes never read a partial file
+                std::vector<dev::NielsD> hG(cap), hH(cap);
+                BPG_HIP(hipMemcpy(hG.data(), gs->G, (size_t)cap * sizeof(dev::NielsD), hipMemcpyDeviceToHost));
+                BPG_HIP(hipMemcpy(hH.data(), gs->H, (size_t)cap * sizeof(dev::NielsD), hipMemcpyDeviceToHost));
+                const std::string path = gens_cache_path(dir, cap);
+                const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+                if (FILE *f = fopen(tmp.c_str(), "wb")) {
+                    const uint64_t hdr[3] = {GENS_MAGIC, cap, gens_checksum(hG, hH)};
+                    bool ok = fwrite(hdr, 8, 3, f) == 3 && fwrite(hG.data(), sizeof(dev::NielsD), cap, f) == cap &&
+                              fwrite(hH.data(), sizeof(dev::NielsD), cap, f) == cap;
+                    ok = (fclose(f) == 0) && ok;
+                    if (!ok || rename(tmp.c_str(), path.c_str()) != 0) remove(tmp.c_str());
+                }
+            }
+        }
+        full = gs;
+        gens_from_cache = loaded;
+        gens_ms += now_ms() - t0;
+    }
+    if (world == 1) return full;
+    auto key = std::make_tuple(N, rank, world);
+    auto it = slices.find(key);
+    if (it != slices.end()) return it->second;
+    std::shared_ptr<GenSet> sl(new GenSet());
+    sl->device = device;
+    sl->N = N / world;
+    sl->rank = rank;
+    sl->world = world;
+    BPG_HIP(hipMalloc(&sl->G, (size_t)sl->N * sizeof(dev::NielsD)));
+    BPG_HIP(hipMalloc(&sl->H, (size_t)sl->N * sizeof(dev::NielsD)));
+    launch_gather_niels(full->G, sl->N, world, rank, sl->G, 0);
+    launch_gather_niels(full->H, sl->N, world, rank, sl->H, 0);
+    BPG_HIP(hipDeviceSynchronize());
+    slices[key] = sl;
+    return sl;
+}
+
+std::shared_ptr<CombTables> DeviceContext::comb(const std::shared_ptr<const GenSet> &gs, uint32_t N) {
+    if (N < 8 || !gs || gs->N < N) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(N, gs->rank, gs->world);
+    auto it = combs.find(key);
+    if (it != combs.end()) return it->second;
+    const double t0 = now_ms();
     const uint32_t h1 = N / 4, ntab = 3 * h1;
     const size_t bytes = (size_t)ntab * 512 * 96;   // per vector
     BPG_HIP(hipSetDevice(device));
-    comb.reset();   // tables for another N are released once their users finish
     size_t free_b = 0, total_b = 0;
     BPG_HIP(hipMemGetInfo(&free_b, &total_b));
     const size_t reserve = std::max<size_t>((size_t)32 << 30, total_b / 8);   // per-thread workspaces
-    if (2 * bytes + reserve > free_b) return nullptr;
+    if (2 * bytes + reserve > free_b) {
+        // evict tables of other sizes that no proof is using
+        for (auto e = combs.begin(); e != combs.end();) {
+            if (e->second.use_count() == 1) e = combs.erase(e);
+            else ++e;
+        }
+        BPG_HIP(hipMemGetInfo(&free_b, &total_b));
+        if (2 * bytes + reserve > free_b) return nullptr;
+    }
     std::shared_ptr<CombTables> t(new CombTables());
     t->device = device;
     t->N = N;
@@ -185,11 +246,12 @@ std::shared_ptr<CombTables> DeviceContext::ensure_comb(uint32_t N) {
         (void)hipGetLastError();
         return nullptr;
     }
-    launch_comb_build(G, h1, ntab, t->tabG, 0);
-    launch_comb_build(H, h1, ntab, t->tabH, 0);
+    launch_comb_build(gs->G, h1, ntab, t->tabG, 0);
+    launch_comb_build(gs->H, h1, ntab, t->tabH, 0);
     BPG_HIP(hipDeviceSynchronize());
-    comb = t;
-    return comb;
+    combs[key] = t;
+    comb_ms += now_ms() - t0;
+    return t;
 }
 
 // ---------------------------------------------------------- instrumentation
@@ -213,7 +275,7 @@ struct Workspace : dev::ProfSink {
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
     DBuf wide, sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
-        ynwR, pts, okflag, wG, wH;
+        ynwR, pts, okflag, wG, wH, wloc, wconv;
     PtD *rows_host = nullptr;        // pinned, 8 x 64 rows
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
@@ -241,7 +303,7 @@ struct Workspace : dev::ProfSink {
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&wide, &sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
-                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag, &wG, &wH};
+                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag, &wG, &wH, &wloc, &wconv};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -285,30 +347,6 @@ struct Workspace : dev::ProfSink {
     }
 };
 
-// Experiment (BPG_CU_SLICES=k, default off): workspace streams restricted to
-// one of k CU slices (stream i -> slice i mod k), so concurrent proofs stop
-// competing for the same CUs; BPG_CU_SLICE_MODE=0 strided mask bits
-// (j mod k == slice), 1 contiguous ranges.
-static void create_workspace_stream(hipStream_t *st) {
-    static const int slices = [] { const char *e = getenv("BPG_CU_SLICES"); return e ? atoi(e) : 0; }();
-    if (slices < 2) {
-        BPG_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
-        return;
-    }
-    static std::atomic<int> counter(0);
-    static const int mode = [] { const char *e = getenv("BPG_CU_SLICE_MODE"); return e ? atoi(e) : 0; }();
-    int dev = 0, ncu = 0;
-    BPG_HIP(hipGetDevice(&dev));
-    BPG_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const int slice = counter.fetch_add(1) % slices;
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int j = 0; j < ncu; j++) {
-        const bool on = mode == 0 ? (j % slices == slice) : (j * slices / ncu == slice);
-        if (on) mask[j / 32] |= 1u << (j % 32);
-    }
-    BPG_HIP(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
-}
-
 Workspace &thread_workspace(int device) {
     static thread_local std::map<int, std::unique_ptr<Workspace>> wss;
     auto &p = wss[device];
@@ -316,7 +354,7 @@ Workspace &thread_workspace(int device) {
         BPG_HIP(hipSetDevice(device));
         p.reset(new Workspace());
         p->device = device;
-        create_workspace_stream(&p->st);
+        BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
         BPG_HIP(hipEventCreateWithFlags(&p->done_ev, hipEventBlockingSync | hipEventDisableTiming));
         p->msm.reset(new MsmEngine(p->st));
         BPG_HIP(hipHostMalloc((void **)&p->rows_host, 8 * 64 * sizeof(PtD), hipHostMallocDefault));
@@ -327,7 +365,7 @@ Workspace &thread_workspace(int device) {
     return *p;
 }
 
-ProveTimings &last_timings() { static ProveTimings t; return t; }   // last proof on any thread
+ProveTimings &last_timings() { static thread_local ProveTimings t; return t; }
 
 template <class T>
 static T *as(DBuf &b) { return reinterpret_cast<T *>(b.p); }
@@ -355,7 +393,8 @@ PreparedCS::~PreparedCS() {
     for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
 }
 
-std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
+std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, const Strategy &strat, uint32_t rank,
+                                       uint32_t world) {
     std::unique_ptr<PreparedCS> P(new PreparedCS());
     BPG_HIP(hipSetDevice(device));
     P->device = device;
@@ -363,8 +402,17 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
     P->N = next_pow2(cs->n);
     P->lgN = lg2u(P->N);
     P->prover = cs->a_L != nullptr;
+    P->strat = strat;
     const uint32_t n = cs->n, m = cs->m;
     if (n >= (1u << 28) || m >= (1u << 28)) throw std::runtime_error("circuit too large");
+    if (world < 1 || (world & (world - 1)) || rank >= world) throw std::runtime_error("bad shard (world must be a power of two)");
+    // the sharded prover keeps at least 8 lanes per rank (the IPP tail needs
+    // a materialised level before the local rounds end)
+    if (world > 1 && (!P->prover || P->N < 8 * world || n < world))
+        throw std::runtime_error("circuit too small to shard over this many ranks");
+    P->rank = rank; P->world = world;
+    P->Nl = P->N / world;
+    P->nl = n > rank ? (n - rank + world - 1) / world : 0;
     // constraint matrix, transposed to columns [L | R | O | V | One]
     const uint32_t ncol = 3 * n + m + 1;
     P->ncol = ncol;
@@ -413,12 +461,15 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
     up(P->short_cols, sc_.data(), sc_.size() * 4);
     up(P->long_cols, lc_.data(), lc_.size() * 4);
     if (P->prover) {
-        std::vector<ScD> tmp(n ? n : 1);
+        // a_L, a_R, a_O: this rank's lanes i = j * world + rank
+        const uint32_t nl = P->nl;
+        std::vector<ScD> tmp(nl ? nl : 1);
         const uint8_t *src[3] = {cs->a_L, cs->a_R, cs->a_O};
         DBuf *dst[3] = {&P->aL, &P->aR, &P->aO};
         for (int k = 0; k < 3; k++) {
-            for (uint32_t i = 0; i < n; i++) tmp[i] = to_dev(Scalar::reduce(src[k] + 32 * (size_t)i));
-            up(*dst[k], tmp.data(), (size_t)n * sizeof(ScD));
+            for (uint32_t j = 0; j < nl; j++)
+                tmp[j] = to_dev(Scalar::reduce(src[k] + 32 * ((size_t)j * world + rank)));
+            up(*dst[k], tmp.data(), (size_t)nl * sizeof(ScD));
         }
         P->v.resize(m); P->vb.resize(m);
         std::vector<ScD> vbd(m ? m : 1);
@@ -433,8 +484,10 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device) {
         up(P->vb_dev, vbd.data(), (size_t)m * sizeof(ScD));
         P->V.resize((size_t)m * 32);
         if (m) gpu_pedersen(device, P->v, P->vb, P->V.data());
-        DeviceContext::get(device).ensure_comb(P->N);   // circuit-independent, outside any timed region
-        DeviceContext::get(device).ensure_wtab(P->N);
+        // circuit-independent, outside any timed region
+        DeviceContext &ctx = DeviceContext::get(device);
+        std::shared_ptr<const GenSet> gs = ctx.gens(P->N, rank, world);
+        if (strat.tables()) ctx.comb(gs, P->Nl);
     }
     return P;
 }
@@ -503,8 +556,9 @@ static ScD *upload_base2(Workspace &ws, int slot, const Scalar &base) {
     BPG_HIP(hipMemcpyAsync(d, h, 40 * sizeof(ScD), hipMemcpyHostToDevice, ws.st));
     return d;
 }
-// out[i] = mont(base^i), i < count, via two 1024-ary levels
-static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t count, DBuf &lo, DBuf &hi, ScD *out) {
+// out[i] = mont(mult * base^i), i < count, via two 1024-ary levels
+static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t count, DBuf &lo, DBuf &hi, ScD *out,
+                       const Scalar &mult = Scalar::one()) {
     uint32_t nhi = count / 1024 + 1;
     lo.grow(1024 * sizeof(ScD));
     hi.grow((size_t)nhi * sizeof(ScD));
@@ -512,10 +566,8 @@ static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t cou
     ScD *b2h = upload_base2(ws, slot + 1, sc_pow_u64(base, 1024));
     launch_pow_table(b2, 0, 1024, as<ScD>(lo), ws.st);
     launch_pow_table(b2h, 0, nhi, as<ScD>(hi), ws.st);
-    if (out) launch_pow_expand(as<ScD>(lo), as<ScD>(hi), count, out, ws.st);
+    if (out) launch_pow_expand(as<ScD>(lo), as<ScD>(hi), count, mont(mult), out, ws.st);
 }
-
-static void check_point_nonidentity(const uint8_t c[32]) { (void)c; }
 
 // ------------------------------------------------------------------- prove
 // Transcript::new(label) + Prover::new + commit(V_i) (prove.rs:45-72 order)
@@ -613,7 +665,7 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
 }
 
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
-                               const uint8_t entropy[32], ProveTimings *tm) {
+                               const uint8_t entropy[32], ProveTimings *tm, const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
     Workspace &ws = thread_workspace(cs.device);
     double t0 = now_ms();
@@ -624,7 +676,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     rng_draw_group(cs, label, label_len, &entropy, 1, &rbp, false);
     double t1 = now_ms();
     ProveTimings t;
-    std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, rb, &t);
+    std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, rb, &t, ag);
     t.rng_ms = t1 - t0;
     t.total_ms += t1 - t0;
     last_timings() = t;
@@ -632,12 +684,46 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     return pr;
 }
 
+// Sharded prover exchanges: every rank's partial points or
+// scalars are all-gathered and summed identically on every rank (a Ristretto
+// point sum is not an RCCL reduction op, so the sum happens on the host).
+static std::vector<Point> allgather_point_sums(const AllGather &ag, const Point *p, int cnt, uint32_t world) {
+    std::vector<uint8_t> send(32 * (size_t)cnt), recv(32 * (size_t)cnt * world);
+    for (int c = 0; c < cnt; c++) ristretto_compress(send.data() + 32 * c, p[c]);
+    ag(send.data(), send.size(), recv.data());
+    std::vector<Point> out(cnt);
+    for (int c = 0; c < cnt; c++) {
+        pt_identity(out[c]);
+        for (uint32_t r = 0; r < world; r++) {
+            Point q, t;
+            if (!ristretto_decompress(q, recv.data() + 32 * ((size_t)r * cnt + c)))
+                throw std::runtime_error("sharded prove: a rank sent an invalid point");
+            pt_add(t, out[c], q);
+            out[c] = t;
+        }
+    }
+    return out;
+}
+static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scalar *s, int cnt, uint32_t world) {
+    std::vector<uint8_t> send(32 * (size_t)cnt), recv(32 * (size_t)cnt * world);
+    for (int c = 0; c < cnt; c++) s[c].to_bytes(send.data() + 32 * c);
+    ag(send.data(), send.size(), recv.data());
+    std::vector<Scalar> out(cnt, Scalar::zero());
+    for (int c = 0; c < cnt; c++)
+        for (uint32_t r = 0; r < world; r++) out[c] = out[c] + Scalar::reduce(recv.data() + 32 * ((size_t)r * cnt + c));
+    return out;
+}
+
 std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
-                                   ProveTimings *tm) {
+                                   ProveTimings *tm, const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t n = cs.n, m = cs.m, N = cs.N, lgN = cs.lgN;
-    ctx.ensure_gens(N);
+    // this rank's slice: lanes i = j * world + rank, j < nl real, j < Nl padded
+    const uint32_t world = cs.world, rank = cs.rank, nl = cs.nl, Nl = cs.Nl;
+    const bool sharded = world > 1;
+    if (sharded && !ag) throw std::runtime_error("sharded prove without an exchange");
+    std::shared_ptr<const GenSet> gs = ctx.gens(N, rank, world);
     Workspace &ws = thread_workspace(cs.device);
     hipStream_t st = ws.st;
     double t0 = now_ms();
@@ -648,49 +734,47 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G> (blinding terms added on the host)
     PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
     MsmPlan pA{}, pS{};
-    // MSM bases for the level-0 generators
-    // (fixed-base window tables when present: all windows of an MSM share one
-    // row of buckets; else affine or affine-Niels generators)
-    std::shared_ptr<WinTables> wt = ctx.ensure_wtab(N);
-    const bool aff = !wt && msm_affine_enabled();
-    const void *G0m = wt ? (const void *)wt->G : aff ? (const void *)ctx.Ga : (const void *)ctx.G;
-    const void *H0m = wt ? (const void *)wt->H : aff ? (const void *)ctx.Ha : (const void *)ctx.H;
-    const int fmt0 = aff ? MSM_AFFINE : MSM_NIELS;
-    const uint32_t ws0 = wt ? wt->N : 0;   // window stride of the level-0 bases
-    if (n) {
-        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0m, n, 0, ws0},
-                          {as<ScD>(const_cast<DBuf &>(cs.aR)), H0m, n, 0, ws0},
-                          {as<ScD>(const_cast<DBuf &>(cs.aO)), G0m, n, 1, ws0}};
-        int ph = ws.prof_begin("msm_commit", 3.0 * n * (64 + 32));
-        pA = ws.msm->enqueue(segA, 3, 2, rowsA, fmt0);
+    const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
+    if (nl) {
+        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0},
+                          {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0},
+                          {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1}};
+        int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
+        pA = ws.msm->enqueue(segA, 3, 2, rowsA, MSM_NIELS);
         ws.prof_end(ph);
     }
-    // s_L | s_R: raw 64-byte draws -> device, reduced mod l there
-    ws.sL.grow((size_t)n * sizeof(ScD) + 64);
-    ws.sR.grow((size_t)n * sizeof(ScD) + 64);
-    ws.wide.grow(2 * (size_t)n * 64 + 64);
-    if (n) {
+    // s_L | s_R: raw 64-byte draws -> device, reduced mod l there (this
+    // rank's lanes only)
+    ws.sL.grow((size_t)nl * sizeof(ScD) + 64);
+    ws.sR.grow((size_t)nl * sizeof(ScD) + 64);
+    if (nl) {
         const uint8_t *wd = rb.wide;
         if (!rb.on_device) {
+            ws.wide.grow(2 * (size_t)n * 64 + 64);
             BPG_HIP(hipMemcpyAsync(ws.wide.p, rb.wide, 2 * (size_t)n * 64, hipMemcpyHostToDevice, st));
             wd = as<uint8_t>(ws.wide);
         }
-        launch_wide_reduce(wd, n, as<ScD>(ws.sL), st);
-        launch_wide_reduce(wd + 64 * (size_t)n, n, as<ScD>(ws.sR), st);
-        MsmSeg segS[2] = {{as<ScD>(ws.sL), G0m, n, 0, ws0}, {as<ScD>(ws.sR), H0m, n, 0, ws0}};
-        int ph = ws.prof_begin("msm_commit", 2.0 * n * (64 + 32));
-        pS = ws.msm->enqueue(segS, 2, 1, rowsS, fmt0);
+        launch_wide_reduce(wd, nl, world, rank, as<ScD>(ws.sL), st);
+        launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(ws.sR), st);
+        MsmSeg segS[2] = {{as<ScD>(ws.sL), G0, nl, 0}, {as<ScD>(ws.sR), H0, nl, 0}};
+        int ph = ws.prof_begin("msm_commit", 2.0 * nl * (64 + 32));
+        pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
         ws.prof_end(ph);
     }
     ws.sync();
-    Point AI, AO, S, tmp;
-    if (n) {
-        combine_rows(AI, rowsA, pA.W, pA.c);
-        combine_rows(AO, rowsA + pA.W, pA.W, pA.c);
-        combine_rows(S, rowsS, pS.W, pS.c);
+    Point AIS[3], tmp;
+    if (nl) {
+        combine_rows(AIS[0], rowsA, pA.W, pA.c);
+        combine_rows(AIS[1], rowsA + pA.W, pA.W, pA.c);
+        combine_rows(AIS[2], rowsS, pS.W, pS.c);
     } else {
-        pt_identity(AI); pt_identity(AO); pt_identity(S);
+        pt_identity(AIS[0]); pt_identity(AIS[1]); pt_identity(AIS[2]);
     }
+    if (sharded) {
+        std::vector<Point> sum = allgather_point_sums(*ag, AIS, 3, world);
+        for (int k = 0; k < 3; k++) AIS[k] = sum[k];
+    }
+    Point &AI = AIS[0], &AO = AIS[1], &S = AIS[2];
     mul_B_blinding(tmp, i_bl); pt_add(AI, AI, tmp);
     mul_B_blinding(tmp, o_bl); pt_add(AO, AO, tmp);
     mul_B_blinding(tmp, s_bl); pt_add(S, S, tmp);
@@ -708,16 +792,19 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     double t1 = now_ms();
 
     // vectors: powers, flattened_constraints(z), l(x)/r(x) coefficients, t(x)
+    // (y^i and y^-i at this rank's lanes: (y^world)^j * y^rank)
     Scalar y_inv = sc_invert(y);
-    ws.ypm.grow((size_t)N * sizeof(ScD));
-    ws.yipm.grow((size_t)N * sizeof(ScD));
+    ws.ypm.grow((size_t)Nl * sizeof(ScD));
+    ws.yipm.grow((size_t)Nl * sizeof(ScD));
     DBuf &lo1 = ws.zlo, &hi1 = ws.zhi;
-    pow_vector(ws, 0, y, N, lo1, hi1, as<ScD>(ws.ypm));
+    pow_vector(ws, 0, sharded ? sc_pow_u64(y, world) : y, Nl, lo1, hi1, as<ScD>(ws.ypm),
+               sharded ? sc_pow_u64(y, rank) : Scalar::one());
     // second set of tables for y^-1 uses gh as temp space for the hi level
     ws.gh.grow(std::max<size_t>((size_t)(N / 1024 + 2) * sizeof(ScD), 64));
     {
         DBuf lo2, hi2;
-        pow_vector(ws, 2, y_inv, N, lo2, hi2, as<ScD>(ws.yipm));
+        pow_vector(ws, 2, sharded ? sc_pow_u64(y_inv, world) : y_inv, Nl, lo2, hi2, as<ScD>(ws.yipm),
+                   sharded ? sc_pow_u64(y_inv, rank) : Scalar::one());
         pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);   // also syncs tables below
         ws.sync();
         if (lo2.p) (void)hipFree(lo2.p);
@@ -727,24 +814,32 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
                as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
                as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
-    int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32 + (double)cs.q * 0 + 36.0 * 1);
+    int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32);
     launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
     ws.partial.grow(1024 * 8 * sizeof(ScD));
     for (uint32_t col : cs.huge_cols)
         launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(ws.zlo), as<ScD>(ws.zhi),
                             as<ScD>(ws.partial), as<ScD>(ws.w), st);
     ws.prof_end(pfl);
-    ScD *wL = as<ScD>(ws.w), *wR = wL + n, *wO = wL + 2 * (size_t)n, *wV = wL + 3 * (size_t)n;
-    for (DBuf *d : {&ws.l1, &ws.r0, &ws.r1, &ws.r3}) d->grow((size_t)n * sizeof(ScD) + 64);
-    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    ScD *wfull = as<ScD>(ws.w);
+    ScD *wV = wfull + 3 * (size_t)n;
+    ScD *wL = wfull, *wR = wfull + n, *wO = wfull + 2 * (size_t)n;
+    if (sharded) {   // w_L, w_R, w_O at this rank's lanes
+        ws.wloc.grow(3 * (size_t)nl * sizeof(ScD) + 64);
+        wL = as<ScD>(ws.wloc); wR = wL + nl; wO = wL + 2 * (size_t)nl;
+        launch_gather_scalars(wfull, nl, world, rank, wL, st);
+        launch_gather_scalars(wfull + n, nl, world, rank, wR, st);
+        launch_gather_scalars(wfull + 2 * (size_t)n, nl, world, rank, wO, st);
+    }
+    for (DBuf *d : {&ws.l1, &ws.r0, &ws.r1, &ws.r3}) d->grow((size_t)nl * sizeof(ScD) + 64);
     ws.small.grow(64 * sizeof(ScD));
     ScD *dsmall = as<ScD>(ws.small);
-    if (n) {
+    if (nl) {
         launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(ws.sR), wL, wR,
-                        wO, as<ScD>(ws.ypm), as<ScD>(ws.yipm), n, as<ScD>(ws.l1), as<ScD>(ws.r0), as<ScD>(ws.r1),
+                        wO, as<ScD>(ws.ypm), as<ScD>(ws.yipm), nl, as<ScD>(ws.l1), as<ScD>(ws.r0), as<ScD>(ws.r1),
                         as<ScD>(ws.r3), st);
         launch_tpoly(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0),
-                     as<ScD>(ws.r1), as<ScD>(ws.r3), n, as<ScD>(ws.partial), dsmall, st);
+                     as<ScD>(ws.r1), as<ScD>(ws.r3), nl, as<ScD>(ws.partial), dsmall, st);
     } else {
         BPG_HIP(hipMemsetAsync(dsmall, 0, 6 * sizeof(ScD), st));
     }
@@ -754,7 +849,11 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     ws.sync();
     Scalar tp[6];
     for (int k = 0; k < 6; k++) tp[k] = from_dev(ws.small_host[1000 + k]);
-    Scalar tb2 = from_dev(ws.small_host[1006]);
+    if (sharded) {
+        std::vector<Scalar> sum = allgather_scalar_sums(*ag, tp, 6, world);
+        for (int k = 0; k < 6; k++) tp[k] = sum[k];
+    }
+    Scalar tb2 = from_dev(ws.small_host[1006]);   // <w_V, v_blinding>: every rank holds all of w_V
     const Scalar tb1 = rb.tb[0], tb3 = rb.tb[1], tb4 = rb.tb[2], tb5 = rb.tb[3], tb6 = rb.tb[4];
     uint8_t cT[5][32];
     pedersen_commit(cT[0], tp[0], tb1);
@@ -783,57 +882,60 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     Point Qp; mul_B(Qp, wch);
     // Q in both base formats: cached for jobs over folded generators, affine
     // Niels for jobs over the level-0 generators
-    ws.Q.grow(sizeof(PtD) + sizeof(NielsD) + sizeof(AffD));
+    ws.Q.grow(sizeof(PtD) + sizeof(NielsD));
     {
-        uint8_t qb[sizeof(PtD) + sizeof(NielsD) + sizeof(AffD)];
+        uint8_t qb[sizeof(PtD) + sizeof(NielsD)];
         pt_to_dev_cached(reinterpret_cast<uint32_t *>(qb), Qp);
         pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD)), Qp);
-        pt_to_dev_affine(reinterpret_cast<uint32_t *>(qb + sizeof(PtD) + sizeof(NielsD)), Qp);
         memcpy(ws.small_host + 3000, qb, sizeof(qb));
         BPG_HIP(hipMemcpyAsync(ws.Q.p, ws.small_host + 3000, sizeof(qb), hipMemcpyHostToDevice, st));
     }
     const PtD *Qc = as<PtD>(ws.Q);
     const NielsD *Qn = reinterpret_cast<const NielsD *>(as<uint8_t>(ws.Q) + sizeof(PtD));
-    const AffD *Qa = reinterpret_cast<const AffD *>(as<uint8_t>(ws.Q) + sizeof(PtD) + sizeof(NielsD));
-    ws.a.grow((size_t)N * sizeof(ScD) + 64);
-    ws.b.grow((size_t)N * sizeof(ScD) + 64);
+    ws.a.grow((size_t)Nl * sizeof(ScD) + 64);
+    ws.b.grow((size_t)Nl * sizeof(ScD) + 64);
     launch_lr_eval(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0), as<ScD>(ws.r1),
-                   as<ScD>(ws.r3), as<ScD>(ws.ypm), n, N, mont(x), mont(x * x), as<ScD>(ws.a), as<ScD>(ws.b), st);
+                   as<ScD>(ws.r3), as<ScD>(ws.ypm), nl, Nl, mont(x), mont(x * x), as<ScD>(ws.a), as<ScD>(ws.b), st);
     double t2 = now_ms();
 
-    // InnerProductProof::create with weighted single-scalar point folding.
-    // With comb tables (N >= 8) rounds 0 and 1 leave the level-1 generators
-    // unmaterialised: round 1's MSM expands them into level-0 generators and
-    // level 2 is built in one table pass.
+    // InnerProductProof::create with weighted single-scalar point folding
+    // over this rank's Nl lanes (a round pairs lane i with i + h, h a
+    // multiple of world, so every local round is rank-local: local half
+    // h / world). With comb tables (Nl >= 8) rounds 0 and 1 leave the level-1
+    // generators unmaterialised: round 1's MSM expands them into level-0
+    // generators and level 2 is built in one table pass.
     T.append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
     T.append_u64("n", N);
-    std::shared_ptr<CombTables> comb = ctx.ensure_comb(N);
+    std::shared_ptr<CombTables> comb = cs.strat.tables() ? ctx.comb(gs, Nl) : nullptr;
     std::vector<uint8_t> LRc(64 * (size_t)lgN);
     Scalar lam = Scalar::one(), mu = Scalar::one();
-    const void *Gh = ctx.G, *Hh = ctx.H;
+    const void *Gh = gs->G, *Hh = gs->H;
     int gfmt = MSM_NIELS;
-    ws.mscal.grow((size_t)(2 * N + 2) * sizeof(ScD) + 64);
-    if (N >= 2) {
-        for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(N / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(N / 2) * sizeof(PtD)); }
+    ws.mscal.grow((size_t)(2 * Nl + 2) * sizeof(ScD) + 64);
+    if (Nl >= 2) {
+        for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(Nl / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(Nl / 2) * sizeof(PtD)); }
     }
     // Round pairs: after round k the fold is left pending (Ghat stays at level
     // k); round k+1's MSM expands each level-(k+1) base into its two level-k
     // points, and level k+2 is built from level k in one pass (comb tables from
     // the level-0 generators, else the three-scalar Straus fold).
-    const bool pairs = fold_pairs_enabled();
+    const bool pairs = cs.strat.pairs();
     Scalar rho_p[4];   // pending fold's scalars (G a/b, H a/b)
     bool pend = false;
     int cur = -1;      // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
     // Tail (DESIGN.md "IPP tail without folds"): once a materialised level is
     // short, the remaining rounds keep it and weight its points instead of
-    // folding them (each fold there is a latency-bound launch).
+    // folding them (each fold there is a latency-bound launch). The sharded
+    // prover always ends in the tail: its last local round's fold is needed
+    // (as weights) for the final generator of each rank.
     static const uint32_t tail_len = [] { const char *e = getenv("BPG_IPP_TAIL"); return e ? (uint32_t)atoi(e) : 4096u; }();
     bool tail = false;
     uint32_t M = 0;
-    uint32_t len = N;
-    for (uint32_t k = 0; len != 1; k++) {
+    uint32_t len = Nl;
+    uint32_t k = 0;
+    for (; len != 1; k++) {
         const uint32_t h = len / 2;
-        if (!tail && !pend && cur >= 0 && len <= tail_len && len >= 4) {
+        if (!tail && !pend && cur >= 0 && len <= tail_len && len >= (sharded ? 2u : 4u)) {
             tail = true;
             M = len;
             ws.wG.grow((size_t)M * sizeof(ScD) + 64);
@@ -842,24 +944,20 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
             launch_fill_scalars(as<ScD>(ws.wH), mont(Scalar::one()), M, st);
         }
         IppRoundArgs A;
-        A.h = h; A.n = n;
+        A.h = h; A.n = nl;
         A.lamG1 = mont(lam); A.lamGu = mont(lam * u);
         A.muH1 = mont(mu); A.muHu = mont(mu * u);
         ScD *ms = as<ScD>(ws.mscal);
-        // MSM bases: the level-0 generators in the MSM format, else Ghat/Hhat
-        const int mfmt = cur < 0 ? fmt0 : MSM_CACHED;
-        const void *Gm = cur < 0 ? G0m : Gh, *Hm = cur < 0 ? H0m : Hh;
-        const void *Qb = mfmt == MSM_NIELS ? (const void *)Qn : mfmt == MSM_AFFINE ? (const void *)Qa : (const void *)Qc;
-        const size_t ps = mfmt == MSM_NIELS ? sizeof(NielsD) : mfmt == MSM_AFFINE ? sizeof(AffD) : sizeof(PtD);
+        // MSM bases: the level-0 generators (affine Niels), else Ghat/Hhat (cached)
+        const int mfmt = cur < 0 ? MSM_NIELS : MSM_CACHED;
+        const void *Gm = cur < 0 ? G0 : Gh, *Hm = cur < 0 ? H0 : Hh;
+        const void *Qb = mfmt == MSM_NIELS ? (const void *)Qn : (const void *)Qc;
+        const size_t ps = mfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
         auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
-        // over window tables, c_L Q and c_R Q leave the job: Q = w B, so they
-        // are (c w) B on the host
-        const uint32_t wsr = cur < 0 ? ws0 : 0;
         MsmSeg seg[10];
         int nseg;
         const bool lazy = pend;
         const size_t hh = h;
-        const ScD *cLR;   // c_L, c_R on the device
         if (tail) {
             launch_ipp_prep_tail(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, M, as<ScD>(ws.wG),
                                  as<ScD>(ws.wH), ms, as<ScD>(ws.partial), st);
@@ -868,66 +966,61 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                             {ms + 2 * mm_, Gh, M, 1}, {ms + 3 * mm_, Hh, M, 1}, {ms + 4 * mm_ + 1, Qb, 1, 1}};
             std::copy(sl, sl + 6, seg);
             nseg = 6;
-            cLR = ms + 4 * mm_;
         } else if (lazy) {
             const uint32_t h0 = 2 * h;
             LazyArgs Z;
             Z.h0 = h0;
             Z.rGa = mont(rho_p[0]); Z.rGb = mont(rho_p[1]); Z.rHa = mont(rho_p[2]); Z.rHb = mont(rho_p[3]);
             launch_ipp_prep_lazy(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
-            MsmSeg sl[10] = {{ms, at(Gm, h), h, 0, wsr}, {ms + hh, at(Gm, h + h0), h, 0, wsr}, {ms + 2 * hh, Hm, h, 0, wsr},
-                             {ms + 3 * hh, at(Hm, h0), h, 0, wsr}, {ms + 8 * hh, Qb, 1, 0},
-                             {ms + 4 * hh, Gm, h, 1, wsr}, {ms + 5 * hh, at(Gm, h0), h, 1, wsr},
-                             {ms + 6 * hh, at(Hm, h), h, 1, wsr}, {ms + 7 * hh, at(Hm, h + h0), h, 1, wsr},
+            MsmSeg sl[10] = {{ms, at(Gm, h), h, 0}, {ms + hh, at(Gm, h + h0), h, 0}, {ms + 2 * hh, Hm, h, 0},
+                             {ms + 3 * hh, at(Hm, h0), h, 0}, {ms + 8 * hh, Qb, 1, 0},
+                             {ms + 4 * hh, Gm, h, 1}, {ms + 5 * hh, at(Gm, h0), h, 1},
+                             {ms + 6 * hh, at(Hm, h), h, 1}, {ms + 7 * hh, at(Hm, h + h0), h, 1},
                              {ms + 8 * hh + 1, Qb, 1, 1}};
-            nseg = 0;
-            for (const MsmSeg &g : sl) if (!(wsr && g.count == 1 && g.base == Qb)) seg[nseg++] = g;
-            cLR = ms + 8 * hh;
+            std::copy(sl, sl + 10, seg);
+            nseg = 10;
         } else {
             launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-            MsmSeg sl[6] = {{ms, at(Gm, h), h, 0, wsr}, {ms + hh, Hm, h, 0, wsr}, {ms + 4 * hh, Qb, 1, 0},
-                            {ms + 2 * hh, Gm, h, 1, wsr}, {ms + 3 * hh, at(Hm, h), h, 1, wsr},
+            MsmSeg sl[6] = {{ms, at(Gm, h), h, 0}, {ms + hh, Hm, h, 0}, {ms + 4 * hh, Qb, 1, 0},
+                            {ms + 2 * hh, Gm, h, 1}, {ms + 3 * hh, at(Hm, h), h, 1},
                             {ms + 4 * hh + 1, Qb, 1, 1}};
-            nseg = 0;
-            for (const MsmSeg &g : sl) if (!(wsr && g.count == 1 && g.base == Qb)) seg[nseg++] = g;
-            cLR = ms + 4 * hh;
+            std::copy(sl, sl + 6, seg);
+            nseg = 6;
         }
         int ph = ws.prof_begin("msm_ipp", ((tail ? 2.0 * M : lazy ? 8.0 * h : 4.0 * h) + 2) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, mfmt);
         ws.prof_end(ph);
-        if (wsr) BPG_HIP(hipMemcpyAsync(ws.small_host + 1020, cLR, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
         ws.sync();
-        Point Lp, Rp;
-        combine_rows(Lp, rowsLR, pl.W, pl.c);
-        combine_rows(Rp, rowsLR + pl.W, pl.W, pl.c);
-        if (wsr) {
-            Point q;
-            mul_B(q, from_dev(ws.small_host[1020]) * wch); pt_add(Lp, Lp, q);
-            mul_B(q, from_dev(ws.small_host[1021]) * wch); pt_add(Rp, Rp, q);
+        Point LR[2];
+        combine_rows(LR[0], rowsLR, pl.W, pl.c);
+        combine_rows(LR[1], rowsLR + pl.W, pl.W, pl.c);
+        if (sharded) {   // c_L Q and c_R Q are inside the partials: sum L and R
+            std::vector<Point> sum = allgather_point_sums(*ag, LR, 2, world);
+            LR[0] = sum[0]; LR[1] = sum[1];
         }
         uint8_t *cl = LRc.data() + 64 * (size_t)k, *cr = cl + 32;
-        ristretto_compress(cl, Lp);
-        ristretto_compress(cr, Rp);
+        ristretto_compress(cl, LR[0]);
+        ristretto_compress(cr, LR[1]);
         T.append_point("L", cl);
         T.append_point("R", cr);
         Scalar uk = T.challenge_scalar("u");
         Scalar uinv = sc_invert(uk);
         launch_ipp_fold_scalars(as<ScD>(ws.a), as<ScD>(ws.b), h, mont(uk), mont(uinv), st);
         Scalar u2 = uk * uk, ui2 = uinv * uinv;
-        Scalar yh = sc_pow_u64(y_inv, h);
+        Scalar yh = sc_pow_u64(y_inv, (uint64_t)h * world);   // the round's global half length
         Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
         const int nxt = cur == 0 ? 1 : 0;
         if (tail) {
-            if (h > 1)
-                launch_ipp_tail_weights(as<ScD>(ws.wG), as<ScD>(ws.wH), M, h, n, mont(rGa), mont(rGb), mont(rHa),
+            if (h > 1 || sharded)
+                launch_ipp_tail_weights(as<ScD>(ws.wG), as<ScD>(ws.wH), M, h, nl, mont(rGa), mont(rGb), mont(rHa),
                                         mont(rHb), st);
         } else if (lazy) {
             pend = false;
             if (h > 1) {
                 // level k+1 from level k-1: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
                 const uint32_t h1 = h, h0 = 2 * h;
-                std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)n - h1, (int64_t)n, (int64_t)n - h0,
-                                            (int64_t)n - h0 - h1};
+                std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)nl - h1, (int64_t)nl, (int64_t)nl - h0,
+                                            (int64_t)nl - h0 - h1};
                 std::vector<uint32_t> starts;
                 for (int64_t c : cut) if (c >= 0 && c < (int64_t)h1) starts.push_back((uint32_t)c);
                 std::sort(starts.begin(), starts.end());
@@ -940,7 +1033,8 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 for (uint32_t r = 0; r < C.nrange; r++) {
                     const uint64_t i = starts[r];
                     C.rstart[r] = (uint32_t)i;
-                    const bool b1 = i < n && i + h1 >= n, b0 = i < n && i + h0 >= n, b0h = i + h1 < n && i + h1 + h0 >= n;
+                    const bool b1 = i < nl && i + h1 >= nl, b0 = i < nl && i + h0 >= nl,
+                               b0h = i + h1 < nl && i + h1 + h0 >= nl;
                     for (int v = 0; v < 2; v++) {
                         const Scalar c1 = r1[2 * v + (b1 ? 1 : 0)];
                         const Scalar c2 = rho_p[2 * v + (b0 ? 1 : 0)];
@@ -955,7 +1049,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                     }
                 }
                 if (table) {
-                    C.gens[0] = ctx.G; C.gens[1] = ctx.H;
+                    C.gens[0] = gs->G; C.gens[1] = gs->H;
                     C.tab[0] = comb->tabG; C.tab[1] = comb->tabH;
                     C.out[0] = ws.Gp[nxt].p; C.out[1] = ws.Hp[nxt].p;
                     C.h1 = h1; C.ntab = 3 * h1;
@@ -974,7 +1068,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 pend = true;
             } else {
                 PtD *Gn = as<PtD>(ws.Gp[nxt]), *Hn = as<PtD>(ws.Hp[nxt]);
-                launch_ipp_fold_points(Gh, Hh, gfmt, h, n, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
+                launch_ipp_fold_points(Gh, Hh, gfmt, h, nl, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
                                        ws.fold_stage, st);
                 Gh = Gn; Hh = Hn;
                 cur = nxt;
@@ -987,8 +1081,73 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     }
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1010, ws.a.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1011, ws.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    Point Gfin, Hfin;   // sharded: this rank's last generator pair (weighted sum of the tail level)
+    if (sharded) {
+        if (!tail) throw std::runtime_error("sharded prove ended outside the IPP tail");
+        ws.wconv.grow(2 * (size_t)M * sizeof(ScD) + 64);
+        ScD *wc = as<ScD>(ws.wconv);
+        launch_from_mont(as<ScD>(ws.wG), M, wc, st);
+        launch_from_mont(as<ScD>(ws.wH), M, wc + M, st);
+        MsmSeg sl[2] = {{wc, Gh, M, 0}, {wc + M, Hh, M, 1}};
+        MsmPlan pl = ws.msm->enqueue(sl, 2, 2, rowsLR, MSM_CACHED);
+        ws.sync();
+        combine_rows(Gfin, rowsLR, pl.W, pl.c);
+        combine_rows(Hfin, rowsLR + pl.W, pl.W, pl.c);
+    }
     ws.sync();
     Scalar fa = from_dev(ws.small_host[1010]), fb = from_dev(ws.small_host[1011]);
+    if (sharded) {
+        // the last lg(world) rounds over one lane per rank (global lane i =
+        // rank), dalek's InnerProductProof::create on the host: true
+        // generators G_i = lam * Gf_i * Ghat_i, H_i = mu * y^-i * Gf_i * Hhat_i
+        const Scalar gf = rank < n ? Scalar::one() : u;
+        Point t;
+        mul_var(t, lam * gf, Gfin); Gfin = t;
+        mul_var(t, mu * sc_pow_u64(y_inv, rank) * gf, Hfin); Hfin = t;
+        std::vector<uint8_t> send(128), recv(128 * (size_t)world);
+        fa.to_bytes(send.data()); fb.to_bytes(send.data() + 32);
+        ristretto_compress(send.data() + 64, Gfin);
+        ristretto_compress(send.data() + 96, Hfin);
+        (*ag)(send.data(), send.size(), recv.data());
+        std::vector<Scalar> va(world), vb(world);
+        std::vector<Point> vG(world), vH(world);
+        for (uint32_t r = 0; r < world; r++) {
+            const uint8_t *p = recv.data() + 128 * (size_t)r;
+            va[r] = Scalar::reduce(p);
+            vb[r] = Scalar::reduce(p + 32);
+            if (!ristretto_decompress(vG[r], p + 64) || !ristretto_decompress(vH[r], p + 96))
+                throw std::runtime_error("sharded prove: a rank sent an invalid generator");
+        }
+        for (uint32_t L = world; L > 1; L /= 2, k++) {
+            const uint32_t h = L / 2;
+            Scalar cL = Scalar::zero(), cR = Scalar::zero();
+            Point Lp, Rp;
+            pt_identity(Lp); pt_identity(Rp);
+            auto madd = [&](Point &acc, const Scalar &s, const Point &p) { Point q, r; mul_var(q, s, p); pt_add(r, acc, q); acc = r; };
+            for (uint32_t i = 0; i < h; i++) {
+                cL = cL + va[i] * vb[h + i];
+                cR = cR + va[h + i] * vb[i];
+                madd(Lp, va[i], vG[h + i]); madd(Lp, vb[h + i], vH[i]);
+                madd(Rp, va[h + i], vG[i]); madd(Rp, vb[i], vH[h + i]);
+            }
+            madd(Lp, cL, Qp); madd(Rp, cR, Qp);
+            uint8_t *cl = LRc.data() + 64 * (size_t)k, *cr = cl + 32;
+            ristretto_compress(cl, Lp);
+            ristretto_compress(cr, Rp);
+            T.append_point("L", cl);
+            T.append_point("R", cr);
+            const Scalar uk = T.challenge_scalar("u"), uinv = sc_invert(uk);
+            for (uint32_t i = 0; i < h; i++) {
+                va[i] = va[i] * uk + va[h + i] * uinv;
+                vb[i] = vb[i] * uinv + vb[h + i] * uk;
+                Point g1, g2, h1, h2;
+                mul_var(g1, uinv, vG[i]); mul_var(g2, uk, vG[h + i]); pt_add(vG[i], g1, g2);
+                mul_var(h1, uk, vH[i]); mul_var(h2, uinv, vH[h + i]); pt_add(vH[i], h1, h2);
+            }
+        }
+        fa = va[0];
+        fb = vb[0];
+    }
     ws.prof_flush();
     double t3 = now_ms();
 
@@ -1013,7 +1172,6 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     t.total_ms = t3 - t0;
     last_timings() = t;
     if (tm) *tm = t;
-    (void)check_point_nonidentity;
     return proof;
 }
 
@@ -1052,7 +1210,7 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     if (lgn >= 32) return 0;
     if (!Scalar::from_canonical(ipp + 64 * lgn, pa) || !Scalar::from_canonical(ipp + 64 * lgn + 32, pb)) return 0;
     if (N != (1u << lgn)) return 0;
-    ctx.ensure_gens(N);
+    std::shared_ptr<const GenSet> gs = ctx.gens(N);
     Workspace &ws = thread_workspace(cs.device);
     hipStream_t st = ws.st;
     ws.tabs.grow(8 * 40 * sizeof(ScD));
@@ -1176,7 +1334,7 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
     const uint64_t j0 = (uint64_t)N * shard / nshards, j1 = (uint64_t)N * (shard + 1) / nshards;
     const uint32_t cnt = (uint32_t)(j1 - j0);
-    MsmSeg seg[3] = {{as<ScD>(ws.gh) + j0, ctx.G + j0, cnt, 0}, {as<ScD>(ws.gh) + N + j0, ctx.H + j0, cnt, 0},
+    MsmSeg seg[3] = {{as<ScD>(ws.gh) + j0, gs->G + j0, cnt, 0}, {as<ScD>(ws.gh) + N + j0, gs->H + j0, cnt, 0},
                      {sscal, ws.pts.p, ns, 0}};
     MsmPlan pl = ws.msm->enqueue(seg, shard == 0 ? 3 : 2, 1, ws.rows_host, MSM_NIELS);
     ws.sync();

@@ -4,8 +4,11 @@
 // operation in HIP kernels (kernels.h) and the Merlin transcript + RNG on the
 // host.
 #pragma once
+#include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -20,11 +23,20 @@ using dev::DBuf;
 using dev::PtD;
 using dev::ScD;
 
-// Per-device state shared by all threads: generator cache in HBM
-// (BulletproofGens::new(N,1) is circuit-independent, so derive once) and the
-// fixed-base tables of PedersenGens.
-// Comb tables of the generators for the IPP's first two rounds:
-// j in [N/4, N) of G and of H, 512 packed affine-Niels entries each.
+// BulletproofGens::new(N, 1) (generators.rs) resident in HBM as affine
+// Niels points, or the slice of it one rank of the sharded prover holds
+// (point j of the set = generator j * world + rank). Immutable once built and
+// shared by reference count: a proof holds its snapshot, so a larger circuit
+// arriving on another thread never frees generators still in use.
+struct GenSet {
+    int device = 0;
+    uint32_t N = 0;                 // points per vector
+    uint32_t rank = 0, world = 1;
+    dev::NielsD *G = nullptr, *H = nullptr;
+    ~GenSet();
+};
+// Comb tables of a generator set for the IPP's first two rounds:
+// points j in [N/4, N) of G and of H, 512 packed affine-Niels entries each.
 struct CombTables {
     int device = 0;
     uint32_t N = 0;
@@ -32,51 +44,48 @@ struct CombTables {
     size_t bytes = 0;
     ~CombTables();
 };
-// Fixed-base window tables of G and H (DESIGN.md "Fixed-base MSMs"):
-// [w * N + j] = 2^(16 w) P_j for w < 16, affine Niels, 4 GB at N = 2^20.
-struct WinTables {
-    int device = 0;
-    uint32_t N = 0;
-    dev::NielsD *G = nullptr, *H = nullptr;
-    ~WinTables();
+// IPP fold strategy, per context (bpg_ctx_set_fold_tables / _pairs): -1
+// automatic (env BPG_FOLD_TABLES / BPG_FOLD_PAIRS = 0 disable, default on),
+// 0 off, 1 on. Proof bytes are identical under every strategy.
+struct Strategy {
+    int fold_tables = -1, fold_pairs = -1;
+    bool tables() const;
+    bool pairs() const;
 };
+// Per-device state shared by all threads: the generator sets and comb
+// tables (circuit-independent, so derived once), the fixed-base tables of
+// PedersenGens.
 struct DeviceContext {
     int device = 0;
     std::mutex mu;
-    uint32_t gens_cap = 0;
-    dev::NielsD *G = nullptr, *H = nullptr;   // gens_cap points each, affine Niels
-    dev::AffD *Ga = nullptr, *Ha = nullptr;   // the same points as affine (x, y): 64-B MSM gathers
+    std::shared_ptr<const GenSet> full;   // the largest full set derived so far
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::shared_ptr<const GenSet>> slices;   // (N, rank, world)
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::shared_ptr<CombTables>> combs;      // (N, rank, world)
     PtD *tabB = nullptr, *tabBb = nullptr;
     PtD *Bb = nullptr;                  // B_blinding as a device point
-    std::shared_ptr<CombTables> comb;   // for one N at a time
+    double gens_ms = 0, comb_ms = 0;    // time spent deriving / building (cold-setup breakdown)
+    bool gens_from_cache = false;
     static DeviceContext &get(int device);
-    void ensure_gens(uint32_t N);       // thread-safe; grows the cache
-    // Tables for circuits of padded size N, built on first use; null when
-    // disabled (bpg_set_fold_tables / BPG_FOLD_TABLES=0), N < 8, or when they
-    // would not fit in free HBM with room left for workspaces.
-    std::shared_ptr<CombTables> ensure_comb(uint32_t N);
-    std::shared_ptr<WinTables> wtab;
-    // Window tables for N generators (null when disabled by bpg_set_msm_fixed /
-    // BPG_MSM_FIXED=0 or when they would not fit in free HBM)
-    std::shared_ptr<WinTables> ensure_wtab(uint32_t N);
+    // Thread-safe. world == 1: a full set with at least N points (grown on
+    // demand); else the N / world points of rank `rank` of BulletproofGens(N).
+    std::shared_ptr<const GenSet> gens(uint32_t N, uint32_t rank = 0, uint32_t world = 1);
+    // Comb tables over the first N points of `gs`, built on first use and
+    // cached per (N, slice); null when N < 8 or when they would not fit in
+    // free HBM (tables not in use are evicted first).
+    std::shared_ptr<CombTables> comb(const std::shared_ptr<const GenSet> &gs, uint32_t N);
 };
-// -1 auto (env BPG_FOLD_TABLES, default on), 0 off, 1 on
-void set_fold_tables(int mode);
-// -1 auto (env BPG_FOLD_PAIRS, default on), 0 off, 1 on
-void set_fold_pairs(int mode);
-// MSM base format for the level-0 generators: -1 auto (env BPG_MSM_AFFINE,
-// default off: measured no throughput gain, profiles/r01j_ab.txt), 0 affine
-// Niels (128 B, 7M adds), 1 affine (64 B, 9M adds)
-void set_msm_affine(int mode);
-// level-0 MSMs over fixed-base window tables: -1 auto (env BPG_MSM_FIXED,
-// default off: 11% slower, the 4 GB of tables defeat the cache reuse of the
-// 256 MB of generators, profiles/r01l_ab.txt), 0 off, 1 on
-void set_msm_fixed(int mode);
+// On-disk cache of the derived generators: directory from
+// bpg_gens_cache_dir() or env BPG_GENS_CACHE; empty = off.
+void set_gens_cache_dir(const char *dir);
 
 // Flattened circuit resident on the device (inputs in HBM before timing).
 struct PreparedCS {
     int device = 0;
     uint32_t n = 0, m = 0, q = 0, N = 1, lgN = 0;
+    // Sharded prover: this rank holds lanes i = j * world + rank
+    // of every length-N vector; nl real lanes (i < n) and Nl = N / world.
+    uint32_t rank = 0, world = 1, nl = 0, Nl = 1;
+    Strategy strat;
     std::vector<Scalar> v, vb;          // high-level witness + blindings
     std::vector<uint8_t> V;             // m x 32 compressed commitments
     bool prover = true;
@@ -93,7 +102,9 @@ struct PreparedCS {
 };
 
 // Build from a view. With cs->a_L == NULL the circuit is verifier-only.
-std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device);
+// world > 1: the prover's witness vectors are uploaded as this rank's slice.
+std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, const Strategy &strat = Strategy(),
+                                       uint32_t rank = 0, uint32_t world = 1);
 
 // Per-thread workspace (stream + buffers), grown on demand.
 struct Workspace;
@@ -121,12 +132,18 @@ ProducerStage &producer_stage(int device);
 // dev_out the s_L | s_R draws go to out[k]->wide as device buffers.
 void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
                     int count, RngBlock *const *out, bool dev_out);
+// Collective of the sharded prover: every rank contributes `bytes` and
+// receives world x bytes in rank order (an all-gather; the caller supplies
+// it, e.g. torch.distributed over RCCL).
+typedef std::function<void(const void *send, size_t bytes, void *recv)> AllGather;
 // Prover::prove. Returns proof bytes (R1CSProof::to_bytes, one-phase layout).
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
-                               const uint8_t entropy[32], ProveTimings *tm = nullptr);
+                               const uint8_t entropy[32], ProveTimings *tm = nullptr, const AllGather *ag = nullptr);
 // Prover::prove after the RNG phase (the device part and the transcript).
+// With cs.world > 1 every rank runs this on its slice and `ag` exchanges the
+// partial sums; all ranks return the same proof bytes.
 std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
-                                   ProveTimings *tm = nullptr);
+                                   ProveTimings *tm = nullptr, const AllGather *ag = nullptr);
 // Verifier::verify; returns 1 accept / 0 reject.
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                const uint8_t *proof, size_t proof_len, const uint8_t entropy[32]);
@@ -140,7 +157,7 @@ void gpu_pedersen(int device, const std::vector<Scalar> &v, const std::vector<Sc
 // Generic MSM test hook.
 int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t n, uint8_t out[32]);
 
-ProveTimings &last_timings();
+ProveTimings &last_timings();   // the calling thread's last proof
 
 // Live kernel instrumentation (bench.py roofline): HIP events around the hot
 // launches on their own stream, resolved after the stream synchronises.

@@ -556,6 +556,37 @@ static Tree parse_tree(const std::vector<std::string> &t, size_t &pos) {
     return out;
 }
 
+// ------------------------------------------- Gadget-API entry points
+// Pattern in the reference's Display form (merkle_tree_gadget.rs:21-29):
+// "W", "I" or "H(<left> <right>)".
+static std::unique_ptr<Pattern> parse_display_pattern(const std::string &s, size_t &pos) {
+    while (pos < s.size() && s[pos] == ' ') pos++;
+    if (pos >= s.size()) throw StatementError("malformed pattern");
+    const char c = s[pos++];
+    if (c == 'W' || c == 'I') return std::unique_ptr<Pattern>(new Pattern{c, nullptr, nullptr});
+    if (c != 'H' || pos >= s.size() || s[pos] != '(') throw StatementError("malformed pattern");
+    pos++;
+    std::unique_ptr<Pattern> p(new Pattern{'H', nullptr, nullptr});
+    p->l = parse_display_pattern(s, pos);
+    p->r = parse_display_pattern(s, pos);
+    while (pos < s.size() && s[pos] == ' ') pos++;
+    if (pos >= s.size() || s[pos] != ')') throw StatementError("malformed pattern");
+    pos++;
+    return p;
+}
+void merkle_tree_assemble(ConstraintSystem &cs, const LC &root, std::vector<LC> inst, std::vector<LC> wit,
+                          const std::string &pattern) {
+    size_t pos = 0;
+    std::unique_ptr<Pattern> p = parse_display_pattern(pattern, pos);
+    while (pos < pattern.size() && pattern[pos] == ' ') pos++;
+    if (pos != pattern.size()) throw StatementError("malformed pattern");
+    LC h = merkle_parse(cs, wit, inst, *p);
+    cs.constrain(h - root);
+}
+void range_proof_assemble(ConstraintSystem &cs, const LC &x, unsigned n, const Scalar *x_assign) {
+    range_proof(cs, x, n, x_assign);
+}
+
 // ------------------------------------------------------- statement driver
 class Statement {
   public:

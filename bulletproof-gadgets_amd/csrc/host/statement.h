@@ -91,6 +91,14 @@ Scalar mimc_hash(const std::vector<uint8_t> &preimage);
 // merkle_tree_gadget.rs:106 evaluated natively).
 Scalar mimc_sponge_native(const std::vector<Scalar> &blocks);
 
+// Gadget-API building blocks over a recorder (the Gadget trait callers of
+// src/gadget.rs:7-60 that build circuits in code, not in the mini-language):
+// MerkleTree256::assemble (merkle_tree_gadget.rs:44-56; `pattern` in the
+// reference's Display form, e.g. "H(H(W W) I)") and utils.rs:5 range_proof.
+void merkle_tree_assemble(ConstraintSystem &cs, const LC &root, std::vector<LC> inst, std::vector<LC> wit,
+                          const std::string &pattern);
+void range_proof_assemble(ConstraintSystem &cs, const LC &x, unsigned n, const Scalar *x_assign);
+
 // Statement drivers (src/prove.rs:37-75, src/verify.rs:36-69).
 struct Synthesis {
     std::unique_ptr<ConstraintSystem> cs;

@@ -1,9 +1,13 @@
 """Multi-GPU plumbing over torch.distributed (RCCL on ROCm; gloo for the CPU
 tests), one process per GPU.
 
-Two uses:
+Three uses:
 * throughput: independent proofs per rank, no data-path collective; the
   bench's barrier and max-over-ranks wall time (`max_over_ranks`);
+* one proof sharded across GPUs (`sharded_prove`): the cyclic lane layout
+  keeps every commitment MSM and the first lg(N/world) IPP rounds
+  rank-local; the partial points/scalars of each step are all-gathered
+  (lg N + 3 small collectives per proof) and summed on every rank;
 * one big verification sharded across GPUs: each rank sums its slice of the
   verifier's mega-MSM (`bpg_r1cs_verify_shard`), the 32-byte partials are
   all-gathered (RCCL has no elliptic-curve reduction op, so a Ristretto point
@@ -46,6 +50,17 @@ def combine_verify(bpg, msgs):
     if any(m[0] != 1 for m in msgs):
         return False
     return bpg.point_sum([m[1:] for m in msgs]) == IDENTITY
+
+
+def sharded_prove(ctx, label, view, entropy):
+    """Prover::prove (prove.rs:79) of ONE proof split over all ranks of the
+    default process group (bpg_r1cs_prove_sharded: rank r holds lanes
+    i = j * world + r; partial sums are all-gathered per exchange). Every
+    rank returns the same (proof, V)."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if world == 1:
+        return ctx.r1cs_prove(label, view, entropy)
+    return ctx.r1cs_prove_sharded(label, view, entropy, rank, world, all_gather_bytes)
 
 
 def sharded_verify(bpg, ctx, label, view, V, proof, entropy=b"\x05" * 32):

@@ -80,32 +80,14 @@ void bpg_clear_seed(void);
 /* Added: select the HIP device used by the calling thread (default 0). */
 int bpg_set_device(int device);
 
-/* Added: IPP fold strategy (process-wide). mode 1: comb tables of the
- * generators (HBM-resident, ~74 KB x N per device) fold rounds 0-1 in one
- * table pass; mode 0: per-round variable-base fold; -1: automatic (tables
- * when they fit in free HBM; env BPG_FOLD_TABLES=0 disables). Proof bytes are
- * identical either way. */
-int bpg_set_fold_tables(int mode);
-
-/* Added: IPP point folds in round pairs (process-wide). mode 1: rounds k, k+1
- * fold together (level k+2 from level k by a three-scalar Straus pass, round
- * k+1's MSM over the level-k points); mode 0: one fold per round; -1:
- * automatic (pairs; env BPG_FOLD_PAIRS=0 disables). Proof bytes are identical
- * either way. */
-int bpg_set_fold_pairs(int mode);
-
-/* Added: MSM base format of the generators (process-wide). mode 1: affine
- * (x, y), 64-B gathers and 9M additions; mode 0: affine Niels, 128-B gathers
- * and 7M additions; -1: automatic (affine Niels; env BPG_MSM_AFFINE=1 selects affine).
- * Proof bytes are identical either way. */
-int bpg_set_msm_affine(int mode);
-
-/* Added: fixed-base window tables for the MSMs over the generators
- * (process-wide). mode 1: 2^(16w) G_j, 2^(16w) H_j for w < 16 resident in HBM
- * (~4 KB x N per device), every window of an MSM shares one row of buckets;
- * mode 0: one bucket row per window; -1: automatic (mode 0; env
- * BPG_MSM_FIXED=1 selects tables). Proof bytes are identical either way. */
-int bpg_set_msm_fixed(int mode);
+/* Added: on-disk cache of the derived generators (BulletproofGens::new,
+ * prove.rs:78 / verify.rs:70). The SHAKE256 generator
+ * chains are serial host work (~1-2 s at N = 2^20); with a cache directory
+ * set, the first process derives and writes `bpg_gens_<N>.bin` there and
+ * later processes load it (checked by a checksum and by recomputing the
+ * first points of both chains). NULL or "" turns the cache off; default:
+ * env BPG_GENS_CACHE, else off. */
+void bpg_gens_cache_dir(const char *dir);
 
 /* ------------------------------------------------------------------------ */
 /* 2. Inner operator ABI: the flattened constraint system                     */
@@ -151,6 +133,24 @@ typedef struct bpg_ctx bpg_ctx;
 bpg_ctx *bpg_ctx_create(int device);
 void bpg_ctx_destroy(bpg_ctx *ctx);
 
+/* IPP fold strategy of the calls made through `ctx` (bpg_r1cs_prove,
+ * bpg_prepare; a prepared circuit keeps the strategy it was prepared with).
+ * Proof bytes are identical under every strategy.
+ *   fold_tables 1: comb tables of the generators (HBM-resident, ~74 KB x N
+ *     per device) fold IPP rounds 0-1 in one table pass; 0: per-round
+ *     variable-base fold; -1 (default): on unless env BPG_FOLD_TABLES=0
+ *     (tables are skipped when they do not fit in free HBM).
+ *   fold_pairs 1: rounds k, k+1 fold together (level k+2 from level k by a
+ *     three-scalar Straus pass); 0: one fold per round; -1 (default): on
+ *     unless env BPG_FOLD_PAIRS=0. */
+int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode);
+int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
+
+/* Cold-setup breakdown of the device `ctx` is on: out[0] ms spent deriving
+ * (or loading) generators, out[1] ms building comb tables, out[2] 1 if the
+ * generators came from the on-disk cache. */
+int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n);
+
 /* Ensure G_i, H_i for i < capacity are resident (BulletproofGens::new(cap,1),
  * bulletproofs@2.1.0 generators.rs). */
 int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity);
@@ -178,6 +178,30 @@ int bpg_r1cs_verify(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
                     const bpg_r1cs_view *cs, const uint8_t *V,
                     const uint8_t *proof, size_t proof_len,
                     const uint8_t entropy[32]);
+
+/* Multi-GPU proving of ONE proof (north_star "the MSM shards
+ * by scalar/point slice across the GPUs"): call on every rank r < world
+ * (world a power of two, N >= 8 * world) with the same arguments. Rank r
+ * holds lanes i = j * world + r of every length-N vector (a_L, a_R, a_O,
+ * s_L, s_R, the generators, l(x), r(x)); an IPP round pairs lane i with
+ * i + N/2^(k+1), a multiple of world, so the commitment MSMs, t(x) and the
+ * first lg(N / world) IPP rounds are rank-local. Exchanges, all 32-byte
+ * values gathered from every rank and summed on the host (a Ristretto sum is
+ * not an RCCL reduction op): the commitment partials (A_I1, A_O1, S1), the
+ * t(x) partials, per IPP round the partial L and R, and once the last
+ * lane's (a, b, G, H); the final lg(world) rounds run on the host. Every
+ * rank runs the transcript and the TranscriptRng itself, so no broadcast is
+ * needed; all ranks return the same proof, byte-identical to
+ * bpg_r1cs_prove's. `allgather(user, send, bytes, recv)` must place every
+ * rank's `bytes` in rank order into recv (world * bytes) and return 0. */
+typedef int (*bpg_allgather_fn)(void *user, const void *send, size_t bytes,
+                                void *recv);
+int bpg_r1cs_prove_sharded(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
+                           const bpg_r1cs_view *cs, const uint8_t entropy[32],
+                           uint32_t rank, uint32_t world,
+                           bpg_allgather_fn allgather, void *user,
+                           uint8_t *proof_out, size_t proof_cap,
+                           size_t *proof_len, uint8_t *V_out);
 
 /* Multi-GPU verification: shard `shard` of `nshards` of
  * Verifier::verify's single mega-MSM. Every shard replays the transcript and
@@ -210,7 +234,10 @@ bpg_prepared *bpg_prepare_verifier(bpg_ctx *ctx, const bpg_r1cs_view *cs);
 
 /* Prove `count` independent proofs of one prepared circuit (proof k uses
  * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
- * host threads sharing the device. lens[k] receives each proof length. */
+ * host threads sharing the device. lens[k] receives each proof length.
+ * Batch calls (this and bpg_verify_batch) run on one process-wide worker
+ * pool: concurrent calls from several threads are safe and run one after
+ * the other. */
 int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len,
                     const uint8_t *entropy, uint32_t count, uint32_t threads,
                     uint8_t *proof_out, size_t proof_stride, size_t *lens);
@@ -226,7 +253,8 @@ int bpg_verify_batch(bpg_prepared *p, const uint8_t *label, size_t label_len,
                      const uint8_t entropy[32], int *results);
 
 /* Per-phase wall-clock timers of the last prove on this thread (ms):
- * [0] transcript+rng, [1] commit MSMs, [2] vectors, [3] IPP, [4] total. */
+ * [0] transcript+rng, [1] commit MSMs, [2] vectors, [3] IPP, [4] total.
+ * After bpg_prove_batch: the batch's last proof. */
 int bpg_last_timings(double *out, int n);
 
 /* Generic device MSM: out = sum scalars[i] * points[i] (compressed in/out).
@@ -252,6 +280,47 @@ const char *bpg_synth_commitments(const bpg_synth *s);
 /* Verifier-side commitments (m x 32 bytes, commit order). */
 const uint8_t *bpg_synth_V(const bpg_synth *s);
 void bpg_synth_free(bpg_synth *s);
+
+/* Gadget-API recorder: the r1cs::ConstraintSystem operations the reference's
+ * Gadget trait callers (src/gadget.rs:7-60, tests/combine_gadgets.rs) issue,
+ * recorded the way ProverBuffer / VerifierBuffer record them
+ * (src/cs_buffer.rs:22-199) and flattened into a bpg_r1cs_view for
+ * bpg_r1cs_prove / bpg_r1cs_verify / bpg_prepare. A Rust caller replays its
+ * buffer (or implements ConstraintSystem over these calls), see
+ * INTEGRATION.md. Variables are BPG_VAR encodings; a linear combination is
+ * `nterms` (variable, 32-byte LE coefficient) pairs; coefficients are kept
+ * as given (LinearCombination's Scalars may be unreduced, e.g. be_to_scalar
+ * of 32 bytes) and reduced where the prover uses them, as dalek does. */
+typedef struct bpg_lc {
+    uint32_t nterms;
+    const uint32_t *vars;
+    const uint8_t *coeffs;   /* nterms x 32 */
+} bpg_lc;
+typedef struct bpg_cs bpg_cs;
+/* prover != 0: r1cs::Prover semantics (assignments evaluated eagerly);
+ * else r1cs::Verifier (variables only, commitments as points). */
+bpg_cs *bpg_cs_create(int prover);
+void bpg_cs_free(bpg_cs *cs);
+/* Prover::commit(v, v_blinding) (v kept as given, Scalar::from_bits) /
+ * Verifier::commit(V): the committed Variable, or < 0 on error. */
+int64_t bpg_cs_commit(bpg_cs *cs, const uint8_t v[32], const uint8_t v_blinding[32]);
+int64_t bpg_cs_commit_point(bpg_cs *cs, const uint8_t V[32]);
+/* ConstraintSystem::multiply / allocate_multiplier (assignment NULL on the
+ * verifier) / constrain. out = (left, right, output) variables. */
+int bpg_cs_multiply(bpg_cs *cs, const bpg_lc *left, const bpg_lc *right, uint32_t out[3]);
+int bpg_cs_allocate_multiplier(bpg_cs *cs, const uint8_t *left, const uint8_t *right, uint32_t out[3]);
+int bpg_cs_constrain(bpg_cs *cs, const bpg_lc *lc);
+/* The crate's gadgets as Gadget-API building blocks on a recorder:
+ * MerkleTree256::assemble (merkle_tree_gadget.rs:44-56; `pattern` in the
+ * reference's Display form, e.g. "H(H(W W) I)") and utils.rs:5 range_proof
+ * (x_assignment NULL on the verifier). */
+int bpg_cs_merkle_tree(bpg_cs *cs, const bpg_lc *root, const bpg_lc *inst, uint32_t ninst,
+                       const bpg_lc *wit, uint32_t nwit, const char *pattern);
+int bpg_cs_range_proof(bpg_cs *cs, const bpg_lc *x, uint32_t bits, const uint8_t *x_assignment);
+/* The flattened system so far (owned by `cs`, valid until the next call on
+ * it); verifier side: bpg_cs_V holds the m committed points. */
+const bpg_r1cs_view *bpg_cs_view(bpg_cs *cs);
+const uint8_t *bpg_cs_V(const bpg_cs *cs);
 
 /* Native MiMC (src/mimc_hash/mimc.rs:61) and the unpadded node sponge
  * (merkle_tree_gadget.rs:106) for building statements (instances/roots). */

@@ -110,32 +110,25 @@ def test_fixture_bit_exact(bpg, resources, name):
     assert S.verify_statement(name.encode(), fx["inst"], proof, coms, fx["gadgets"])
 
 
-@pytest.mark.parametrize("mode,pairs,aff,fixed", [(0, 0, 0, 0), (1, 0, 1, 0), (0, 1, 0, 1), (1, 1, 0, 1), (1, 1, 1, 0)])
+@pytest.mark.parametrize("tables,pairs", [(0, 0), (1, 0), (0, 1), (1, 1), (-1, -1)])
 @pytest.mark.parametrize("name", ["bounds_check", "less_than", "example", "inequality", "or5"])
-def test_fold_strategy_bit_exact(bpg, resources, name, mode, pairs, aff, fixed):
-    """Every IPP fold strategy and generator MSM form (affine / affine Niels
-    bases, fixed-base window tables; per-round variable-base fold; comb-table pass
-    for rounds 0-1 with a lazily expanded round-1 MSM; round pairs folded by
-    the three-scalar Straus pass with lazily expanded odd-round MSMs) gives
-    the oracle's bytes. The fixtures put n - N/2 on both sides of N/4, so
+def test_fold_strategy_bit_exact(bpg, resources, name, tables, pairs):
+    """Every IPP fold strategy of a context (per-round variable-base fold;
+    comb-table pass for rounds 0-1 with a lazily expanded round-1 MSM; round
+    pairs folded by the three-scalar Straus pass with lazily expanded
+    odd-round MSMs; the default) gives the oracle's bytes through the inner
+    ABI (bpg_r1cs_prove). The fixtures put n - N/2 on both sides of N/4, so
     every lane class of the two-round passes occurs."""
     fx = read_fixture(os.path.join(resources, name))
     seed = 900 + len(name)
-    lib = bpg.lib()
-    assert lib.bpg_set_fold_tables(mode) == 0
-    assert lib.bpg_set_fold_pairs(pairs) == 0
-    assert lib.bpg_set_msm_affine(aff) == 0
-    assert lib.bpg_set_msm_fixed(fixed) == 0
-    try:
-        bpg.set_seed(seed)
-        proof, coms = bpg.prove(name, fx["inst"], fx["wtns"], fx["gadgets"])
-    finally:
-        lib.bpg_set_fold_tables(-1)
-        lib.bpg_set_fold_pairs(-1)
-        lib.bpg_set_msm_affine(-1)
-        lib.bpg_set_msm_fixed(-1)
-    o_proof, o_coms, _ = S.prove_statement(name.encode(), fx["inst"], fx["wtns"], fx["gadgets"], seed)
-    assert coms == o_coms
+    st = S.synthesize_prover(fx["inst"], fx["wtns"], fx["gadgets"], seed)
+    flat = st.cs.to_flat()
+    ent = S.entropy_for(st)
+    o_proof, o_V = O.r1cs_prove(name.encode(), flat, ent)
+    c = bpg.Context(0)
+    c.set_strategy(tables, pairs)
+    proof, V = c.r1cs_prove(name.encode(), flat.view(), ent)
+    assert V == o_V
     assert proof == o_proof
 
 

@@ -3,12 +3,13 @@ size-independent properties (the oracle is far too slow there):
 
 * a proof produced by the product verifies on the device, and a tampered
   proof or a wrong transcript label does not;
-* the two IPP fold strategies (comb-table pass vs per-round fold) give
-  identical proof bytes — two different algorithms agreeing on every L_k, R_k;
+* every IPP fold strategy, the production default included, gives the same
+  proof bytes — different algorithms agreeing on every L_k, R_k;
 * batched proving (lockstep TranscriptRng producers) equals single proving.
 
 Config 3 (2^16) is additionally compared byte-for-byte with the CPU oracle
-(a few seconds of oracle work).
+(a few seconds of oracle work); configs 4 and 5 and the reference's 2^20
+merkle512 circuit against committed oracle proofs in test_gpu_fullsize.py.
 """
 import ctypes
 import os
@@ -61,41 +62,42 @@ def test_config3_bit_exact_vs_oracle(bpg, ctx, W):
 
 
 @pytest.mark.parametrize("cfg", [3, 4, 5])
-def test_full_size_verify_and_strategies(bpg, ctx, W, cfg):
+def test_full_size_verify_and_strategies(bpg, W, cfg):
     inst, wit, gad = W.CONFIGS[cfg]()
     bpg.set_seed(100 + cfg)
     syn = bpg.Synth(inst, wit, gad)
     ent = bytes([cfg]) * 32
-    lib = bpg.lib()
     proofs = []
-    # (comb tables, round-pair folds): table pass + Straus pair folds, Straus
-    # pair folds only, one variable-base fold per round
-    # and affine / affine-Niels / window-table generator bases in the MSMs
-    for tables, pairs, aff, fixed in ((1, 1, 0, 1), (0, 1, 1, 0), (0, 0, 0, 0)):
-        assert lib.bpg_set_fold_tables(tables) == 0
-        assert lib.bpg_set_fold_pairs(pairs) == 0
-        assert lib.bpg_set_msm_affine(aff) == 0
-        assert lib.bpg_set_msm_fixed(fixed) == 0
-        try:
-            p, V = ctx.r1cs_prove(b"scale", syn.view, ent)
-        finally:
-            lib.bpg_set_fold_tables(-1)
-            lib.bpg_set_fold_pairs(-1)
-            lib.bpg_set_msm_affine(-1)
-            lib.bpg_set_msm_fixed(-1)
+    # (comb tables, round-pair folds): the production default, table pass +
+    # Straus pair folds, Straus pair folds only, one variable-base fold per
+    # round; each through its own context (strategies are per context)
+    for tables, pairs in ((-1, -1), (1, 1), (0, 1), (0, 0)):
+        c = bpg.Context(0)
+        c.set_strategy(tables, pairs)
+        p, V = c.r1cs_prove(b"scale", syn.view, ent)
         proofs.append(p)
-    assert proofs[0] == proofs[1] == proofs[2]
+    assert proofs[0] == proofs[1] == proofs[2] == proofs[3]
     proof = proofs[0]
     N = 1
     while N < syn.n:
         N *= 2
-    assert len(proof) == 417 + 64 * (N.bit_length() - 1)
+    lgN = N.bit_length() - 1
+    assert len(proof) == 417 + 64 * lgN
+    ctx = bpg.Context(0)
     assert V == _V(ctx, syn)
     assert ctx.r1cs_verify(b"scale", syn.view, V, proof)
     assert not ctx.r1cs_verify(b"scalf", syn.view, V, proof)
-    bad = bytearray(proof)
-    bad[417 + 64 * 3 + 5] ^= 4      # inside L_3
-    assert not ctx.r1cs_verify(b"scale", syn.view, V, bytes(bad))
+    # proof layout (R1CSProof::to_bytes, one-phase): version byte, A_I1, A_O1,
+    # S1, T_1, T_3..T_6 (8 points), t_x, t_x_blinding, e_blinding, then
+    # (L_k, R_k) for k < lg N, then a, b
+    ipp = 1 + 8 * 32 + 3 * 32
+    for pos in (ipp + 64 * 3 + 5,          # inside L_3
+                ipp + 64 * (lgN - 1) + 40,  # inside R of the last round
+                1 + 9 * 32 + 3,             # t_x_blinding
+                len(proof) - 1):            # b
+        bad = bytearray(proof)
+        bad[pos] ^= 4
+        assert not ctx.r1cs_verify(b"scale", syn.view, V, bytes(bad))
 
 
 def test_config5_batch_equals_single(bpg, ctx, W):
@@ -130,9 +132,10 @@ def test_sharded_verify(bpg, ctx, W, nshards):
         return bpg.point_sum([m[1:] for m in msgs]) == b"\0" * 32
 
     assert verdict(proof)
+    ipp = 1 + 8 * 32 + 3 * 32  # version, 8 points, t_x, t_x_blinding, e_blinding
     bad = bytearray(proof)
-    bad[417 + 5] ^= 1          # inside L_0
+    bad[ipp + 5] ^= 1          # inside L_0
     assert not verdict(bytes(bad))
     bad = bytearray(proof)
-    bad[300] ^= 1              # t_x
+    bad[1 + 8 * 32 + 3] ^= 1   # t_x
     assert not verdict(bytes(bad))
