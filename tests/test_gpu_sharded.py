@@ -86,9 +86,12 @@ def test_sharded_prove_bit_exact(bpg, tmp_path, name, world):
 
 
 def test_sharded_prove_rejects_small_circuit(bpg):
-    """N < 8 * world is refused (the local rounds must end in the IPP tail)."""
+    """N < 8 * world is refused (the local rounds must end in the IPP tail):
+    bounds_check has n = 1440, N = 2048 < 8 * 512."""
     fx = read_fixture(os.path.join(ROOT, "tests", "golden", "resources", "bounds_check"))
     bpg.set_seed(1)
     syn = bpg.Synth(fx["inst"], fx["wtns"], fx["gadgets"])
     with pytest.raises(bpg.BpgError):
-        bpg.Context(0).r1cs_prove_sharded(b"x", syn.view, bytes(32), 0, 64, lambda p: [p] * 64)
+        bpg.Context(0).r1cs_prove_sharded(b"x", syn.view, bytes(32), 0, 512, lambda p: [p] * 512)
+    with pytest.raises(bpg.BpgError):
+        bpg.Context(0).r1cs_prove_sharded(b"x", syn.view, bytes(32), 0, 3, lambda p: [p] * 3)   # not a power of 2
