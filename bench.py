@@ -142,12 +142,26 @@ def cpu_baseline(leaves, procs):
             "host": {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": _cpu_model()}}
 
 
+def heartbeat(period=20.0):
+    """A progress line on stderr every `period` seconds: the long timed
+    region is one library call and prints nothing else."""
+    import threading
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print("bench: running, %.0f s" % (time.perf_counter() - t0), file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] == "--cpu-sample-child":
         q, dt, _ = _cpu_sample(int(sys.argv[2]))
         print(json.dumps({"q": q, "s": dt}))
         return
     a = parse()
+    heartbeat()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
