@@ -289,6 +289,7 @@ struct Workspace : dev::ProfSink {
         event_wait(done_ev);
     }
     ~Workspace() {
+        for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (done_ev) (void)hipEventDestroy(done_ev);
         if (fold_stage.dev) (void)hipFree(fold_stage.dev);
         if (fold_stage.host) (void)hipHostFree(fold_stage.host);
@@ -309,12 +310,22 @@ struct Workspace : dev::ProfSink {
         if (st) (void)hipStreamDestroy(st);
     }
     std::vector<PendingEvent> pend;
+    // timing events, created once per workspace and reused after every flush
+    // (no hipEventCreate / hipEventDestroy per bracketed launch)
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_next = 0;
+    hipEvent_t take_event() {
+        if (ev_next == ev_pool.size()) {
+            hipEvent_t e;
+            BPG_HIP(hipEventCreate(&e));
+            ev_pool.push_back(e);
+        }
+        return ev_pool[ev_next++];
+    }
     // bracket the launches issued between begin() and end() on `st`
     int prof_begin(const char *name, double bytes, double femul = 0) {
         if (!g_prof) return -1;
-        PendingEvent e{name, nullptr, nullptr, bytes, femul};
-        BPG_HIP(hipEventCreate(&e.a));
-        BPG_HIP(hipEventCreate(&e.b));
+        PendingEvent e{name, take_event(), take_event(), bytes, femul};
         BPG_HIP(hipEventRecord(e.a, st));
         pend.push_back(e);
         return (int)pend.size() - 1;
@@ -334,10 +345,9 @@ struct Workspace : dev::ProfSink {
                 k.alg_bytes += e.bytes;
                 k.femul += e.femul;
             }
-            (void)hipEventDestroy(e.a);
-            (void)hipEventDestroy(e.b);
         }
         pend.clear();
+        ev_next = 0;
     }
     void stage(size_t bytes) {
         if (bytes <= s_host_cap) return;
