@@ -51,9 +51,10 @@ def parse():
                     help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
                          "one HIP stream each (default 24 with >= 16 cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("prove", "verify"), default="prove",
+    ap.add_argument("--mode", choices=("prove", "verify", "latency"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
-                         "(config 5's batch verification; a secondary line, not the headline metric)")
+                         "(config 5's batch verification); latency: one proof at a time, sharded over all "
+                         "ranks (bpg_prove_prepared). Secondary lines, not the headline metric")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="processes of the all-core CPU leg (default: the host cores this rank may use, at most 16)")
@@ -172,7 +173,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        # RCCL between GPUs; BENCH_DIST_BACKEND=gloo lets several ranks share
+        # one GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import workloads as W
     bpg = W._bpg()
     sys.path.insert(0, os.path.join(ROOT, "bulletproof-gadgets_amd"))
@@ -192,6 +199,8 @@ def main():
     bpg.set_seed(1000 + rank)
     syn = bpg.Synth(inst, wit, gad)
     ctx = bpg.Context(dev)
+    if a.mode == "latency":
+        return bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W)
     # cold setup, outside the timed region: BulletproofGens::new (prove.rs:78,
     # derived on the device) and the circuit upload (the IPP comb tables are
     # built by the first warm-up batch, ~0.9 s)
@@ -382,6 +391,60 @@ def bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropie
                    "parallelism": "independent verifications per GPU (%d ranks)" % world},
         "proofs_per_s": round(total / dt, 2),
         "latency_ms_single_verify": round(single_ms, 2),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W):
+    """Single-proof latency of Prover::prove (prove.rs:79) with ONE proof
+    split over all ranks (bpg_prepare_shard + bpg_prove_prepared,
+    cyclic lane layout, partial sums all-gathered over torch.distributed).
+    A step = one proof; value = q / (max-over-ranks seconds per proof).
+    The serial TranscriptRng chain (2n Keccak-f on one host core, run by
+    every rank) is part of every proof and does not shrink with ranks."""
+    import torch
+    q, n = syn.q, syn.n
+    N = 1
+    while N < n:
+        N *= 2
+    tp = time.perf_counter()
+    prep = ctx.prepare_shard(syn.view, rank, world)
+    prepare_ms = (time.perf_counter() - tp) * 1e3
+    ag = D.all_gather_bytes if world > 1 else None
+
+    def ent(k):
+        return (k + 1).to_bytes(32, "little")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for s in range(a.warmup):
+        prep.prove_one(b"bench", ent(10000 + s), ag)
+    barrier()
+    t0 = time.perf_counter()
+    proofs = [prep.prove_one(b"bench", ent(s), ag) for s in range(a.steps)]
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        dt = D.max_over_ranks(dt)
+    phases = bpg.last_timings()
+    if rank == 0 and not ctx.r1cs_verify(b"bench", syn.view, _commitments(ctx, syn), proofs[-1]):
+        raise SystemExit("bench: a sharded proof failed to verify")
+    out = {
+        "metric": "R1CS single-proof latency constraints/sec at %d MI355X (one proof sharded over the ranks)" % world,
+        "value": round(a.steps * q / dt, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32 (255-bit integer field/scalar arithmetic)",
+        "data": "synthetic: seeded config-%d statement" % a.config,
+        "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
+                   "parallelism": "one proof sharded over %d ranks (lanes i = j*%d + rank)" % (world, world)},
+        "latency_ms": round(dt / a.steps * 1e3, 1), "phase_ms_last_proof_rank0": phases,
+        "prepare_ms": round(prepare_ms, 1),
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

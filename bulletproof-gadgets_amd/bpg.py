@@ -30,7 +30,8 @@ EXPORTS = [
     "bpg_verify_batch", "bpg_prepare_verifier", "bpg_gens_cache_dir", "bpg_ctx_set_fold_tables",
     "bpg_ctx_set_fold_pairs", "bpg_ctx_setup_stats", "bpg_r1cs_prove_sharded", "bpg_cs_create", "bpg_cs_free",
     "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
-    "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V",
+    "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
+    "bpg_prove_prepared",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -114,6 +115,9 @@ def lib():
         L.bpg_synth_V.restype = vp
         L.bpg_synth_V.argtypes = [vp]
         L.bpg_synth_free.argtypes = [vp]
+        L.bpg_prepare_shard.restype = vp
+        L.bpg_prepare_shard.argtypes = [vp, vp, u32, u32]
+        L.bpg_prove_prepared.argtypes = [vp, vp, sz, vp, ALLGATHER_FN, vp, vp, sz, ctypes.POINTER(sz)]
         L.bpg_cs_create.restype = vp
         L.bpg_cs_create.argtypes = [ctypes.c_int]
         L.bpg_cs_free.argtypes = [vp]
@@ -364,17 +368,7 @@ class Context:
     def r1cs_prove_sharded(self, label, view, entropy, rank, world, allgather):
         """One proof sharded over `world` ranks (bpg_r1cs_prove_sharded).
         allgather(payload bytes) -> list of every rank's payload, rank order."""
-        err = []
-
-        def cb(_user, send, nbytes, recv):
-            try:
-                parts = allgather(ctypes.string_at(send, nbytes))
-                ctypes.memmove(recv, b"".join(parts), nbytes * world)
-                return 0
-            except Exception as e:  # the library turns a failed exchange into an error status
-                err.append(e)
-                return -1
-        fn = ALLGATHER_FN(cb)
+        fn, err = _allgather_cb(allgather, world)
         out = ctypes.create_string_buffer(MAX_PROOF)
         plen = ctypes.c_size_t(0)
         V = ctypes.create_string_buffer(32 * max(view.m, 1))
@@ -401,6 +395,14 @@ class Context:
             raise BpgError(last_error())
         return rc == 1, part.raw
 
+    def prepare_shard(self, view, rank, world):
+        """bpg_prepare_shard: this rank's slice resident in HBM, for
+        Prepared.prove_one (world == 1: the whole circuit)."""
+        p = lib().bpg_prepare_shard(self.h, ctypes.addressof(view), rank, world)
+        if not p:
+            raise BpgError(last_error())
+        return Prepared(p, world)
+
     def prepare(self, view, verifier=False):
         """HBM-resident circuit: for prove_batch, or with verifier=True for
         verify_batch (bpg_prepare_verifier)."""
@@ -417,9 +419,36 @@ class Context:
             pass
 
 
+def _allgather_cb(allgather, world):
+    """bpg_allgather_fn over a Python allgather(bytes) -> [bytes per rank]."""
+    err = []
+
+    def cb(_user, send, nbytes, recv):
+        try:
+            parts = allgather(ctypes.string_at(send, nbytes))
+            ctypes.memmove(recv, b"".join(parts), nbytes * world)
+            return 0
+        except Exception as e:  # the library turns a failed exchange into an error status
+            err.append(e)
+            return -1
+    return ALLGATHER_FN(cb), err
+
+
 class Prepared:
-    def __init__(self, h):
+    def __init__(self, h, world=1):
         self.h = h
+        self.world = world
+
+    def prove_one(self, label, entropy, allgather=None):
+        """bpg_prove_prepared: one proof on the calling thread (sharded when
+        prepared with world > 1: every rank calls it, allgather exchanges)."""
+        fn, err = _allgather_cb(allgather or (lambda p: [p]), self.world)
+        out = ctypes.create_string_buffer(MAX_PROOF)
+        plen = ctypes.c_size_t(0)
+        rc = lib().bpg_prove_prepared(self.h, label, len(label), entropy, fn, None, out, MAX_PROOF, ctypes.byref(plen))
+        if rc != 0:
+            raise BpgError(last_error() + ("" if not err else " (%r)" % err[0]))
+        return out.raw[:plen.value]
 
     def prove_batch(self, label, entropies, threads):
         count = len(entropies)

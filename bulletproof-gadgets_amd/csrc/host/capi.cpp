@@ -260,6 +260,31 @@ bpg_prepared *bpg_prepare_verifier(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
     return bpg_prepare(ctx, &v);
 }
 void bpg_prepared_free(bpg_prepared *p) { delete p; }
+bpg_prepared *bpg_prepare_shard(bpg_ctx *ctx, const bpg_r1cs_view *cs, uint32_t rank, uint32_t world) {
+    return guarded([&]() -> bpg_prepared * {
+        if (!cs->a_L) throw std::runtime_error("prover view without witness");
+        bpg_prepared *b = new bpg_prepared();
+        b->p = prepare_cs(cs, ctx->device, ctx->strat, rank, world);
+        return b;
+    }, (bpg_prepared *)nullptr);
+}
+int bpg_prove_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len, const uint8_t entropy[32],
+                       bpg_allgather_fn allgather, void *user, uint8_t *proof_out, size_t proof_cap,
+                       size_t *proof_len) {
+    return guarded([&]() -> int {
+        const PreparedCS &cs = *p->p;
+        if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
+        if (cs.world > 1 && !allgather) throw std::runtime_error("sharded circuit without an all-gather");
+        AllGather ag = [&](const void *send, size_t bytes, void *recv) {
+            if (allgather(user, send, bytes, recv) != 0) throw std::runtime_error("all-gather failed");
+        };
+        std::vector<uint8_t> proof = gpu_prove(cs, label, label_len, entropy, nullptr, cs.world > 1 ? &ag : nullptr);
+        if (proof.size() > proof_cap) throw std::runtime_error("proof buffer too small");
+        memcpy(proof_out, proof.data(), proof.size());
+        *proof_len = proof.size();
+        return 0;
+    }, -1);
+}
 
 // Persistent host worker pool: each worker owns its thread-local device
 // workspace (stream + buffers), so repeated batches reuse HBM allocations.

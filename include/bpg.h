@@ -232,6 +232,16 @@ void bpg_prepared_free(bpg_prepared *p);
  * column, Variable::One, that Verifier::verify flattens). */
 bpg_prepared *bpg_prepare_verifier(bpg_ctx *ctx, const bpg_r1cs_view *cs);
 
+/* bpg_r1cs_prove_sharded with the circuit prepared once (HBM-resident) for
+ * repeated single-proof proving: bpg_prepare_shard uploads this rank's slice
+ * (world == 1: the whole circuit), bpg_prove_prepared proves one proof on the
+ * calling thread (TranscriptRng included); `allgather` may be NULL when
+ * world == 1. */
+bpg_prepared *bpg_prepare_shard(bpg_ctx *ctx, const bpg_r1cs_view *cs, uint32_t rank, uint32_t world);
+int bpg_prove_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len,
+                       const uint8_t entropy[32], bpg_allgather_fn allgather, void *user,
+                       uint8_t *proof_out, size_t proof_cap, size_t *proof_len);
+
 /* Prove `count` independent proofs of one prepared circuit (proof k uses
  * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
  * host threads sharing the device. lens[k] receives each proof length.
