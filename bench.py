@@ -69,17 +69,19 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 FEMUL_PEAK_G = 263.5         # GF(2^255-19) multiplies/s x1e9, measured (profiles/*_micro.log, fe_variants V2)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/*_pmc.json, scripts/pmc_summary.py: FETCH_SIZE x 2 per
-    the gfx950 correction + WRITE_SIZE, separate passes), or None."""
+def pmc_row(kernel):
+    """The committed rocprofv3 PMC row of `kernel` (profiles/*_pmc.json, the
+    latest; scripts/pmc_table.py: FETCH_SIZE x 2 per the gfx950 correction +
+    WRITE_SIZE, and the SQ issue counters, separate passes), or {}."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
-        return None
+        return {}
     d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k["hbm_bytes_per_launch"]
+    row = dict(d.get("kernels", {}).get(kernel) or {})
+    if row:
+        row["source"] = os.path.relpath(files[-1], ROOT)
+    return row
 
 
 def _cpu_sample(leaves):
@@ -195,8 +197,11 @@ def main():
     # continuous pipeline (below), so the end-of-batch drain is paid once
     batch = a.batch or 16 * threads
 
-    inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * rank)
-    bpg.set_seed(1000 + rank)
+    # every rank proves its own statement, except in latency mode, where the
+    # ranks share ONE proof of one statement
+    srank = 0 if a.mode == "latency" else rank
+    inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * srank)
+    bpg.set_seed(1000 + srank)
     syn = bpg.Synth(inst, wit, gad)
     ctx = bpg.Context(dev)
     if a.mode == "latency":
@@ -288,18 +293,24 @@ def main():
         lc, ms, by, fm = kernels[dom]
         sec = ms / lc / 1e3                      # average launch duration
         achieved = (by / lc) / sec / 1e9         # GB/s of algorithmic bytes
-        pmc = pmc_traffic(KERNELS[dom])
+        pmc = pmc_row(KERNELS[dom])
         roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm",
                 # the HBM fraction is the metric's; the kernel is limited by its
                 # GF(p) multiply rate and gather latency, see "valu"
                 "limiter": "valu+gather-latency", "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": pmc, "launches": lc, "avg_launch_ms": round(sec * 1e3, 4),
+                "traffic": pmc.get("hbm_bytes_per_launch"), "launches": lc, "avg_launch_ms": round(sec * 1e3, 4),
                 "alg_bytes_per_launch": round(by / lc, 1),
                 # the kernels are VALU-bound (255-bit field arithmetic): the same
                 # launches against the measured GF(p) multiply peak
                 "valu": {"unit": "G fe_mul/s", "achieved": round(fm / lc / sec / 1e9, 2), "peak": FEMUL_PEAK_G,
-                         "frac": round(fm / lc / sec / 1e9 / FEMUL_PEAK_G, 4)},
+                         "frac": round(fm / lc / sec / 1e9 / FEMUL_PEAK_G, 4),
+                         "note": "per-launch time under the bench's concurrency (other streams share the CUs)"},
+                # the same kernel in isolation (PMC passes serialise dispatches):
+                # SQ_ACTIVE_INST_VALU share of the SIMDs' cycles, HBM GB/s
+                "pmc_isolated": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()
+                                 if k in ("avg_us", "valu_issue_share", "avg_waves_per_simd", "wave_wait_mem",
+                                          "hbm_gbs", "clock_ghz", "source")} or None,
                 "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
                 "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items() if v}}
 

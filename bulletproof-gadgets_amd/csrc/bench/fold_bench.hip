@@ -85,30 +85,6 @@ int main(int argc, char **argv) {
     BPG_HIP(hipEventSynchronize(e1));
     BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
     printf("msm job 4h=%u points (Niels bases): %.3f ms per job\n", 4 * h, ms / reps);
-    {   // the same job over affine (x, y) copies of the bases
-        AffD *Ga, *Ha;
-        BPG_HIP(hipMalloc(&Ga, (size_t)2 * h * sizeof(AffD))); BPG_HIP(hipMalloc(&Ha, (size_t)2 * h * sizeof(AffD)));
-        launch_to_affine(G, Ga, 2 * h, st); launch_to_affine(H, Ha, 2 * h, st);
-        MsmSeg sega[4] = {{dsc, Ga + h, h, 0}, {dsc + h, Ha, h, 0}, {dsc + 2 * (size_t)h, Ga, h, 1}, {dsc + 3 * (size_t)h, Ha + h, h, 1}};
-        eng.enqueue(sega, 4, 2, rows, MSM_AFFINE);
-        BPG_HIP(hipStreamSynchronize(st));
-        std::vector<PtD> r1(128);
-        memcpy(r1.data(), rows, 64 * sizeof(PtD));
-        eng.enqueue(seg, 4, 2, rows, MSM_NIELS);
-        BPG_HIP(hipStreamSynchronize(st));
-        int same = 1;
-        for (int i = 0; i < 32; i++) {   // window rows must be the same group elements
-            bpg::Point a, b; bpg::pt_from_dev(a, r1[i].v); bpg::pt_from_dev(b, rows[i].v);
-            uint8_t ca[32], cb[32]; bpg::ristretto_compress(ca, a); bpg::ristretto_compress(cb, b);
-            same &= memcmp(ca, cb, 32) == 0;
-        }
-        BPG_HIP(hipEventRecord(e0, st));
-        for (int k = 0; k < reps; k++) eng.enqueue(sega, 4, 2, rows, MSM_AFFINE);
-        BPG_HIP(hipEventRecord(e1, st));
-        BPG_HIP(hipEventSynchronize(e1));
-        BPG_HIP(hipEventElapsedTime(&ms, e0, e1));
-        printf("msm job 4h=%u points (affine bases): %.3f ms per job; rows match Niels job: %d\n", 4 * h, ms / reps, same);
-    }
     // cached bases (folded generators), round-2 shape: 4 x h/4 points
     const uint32_t q = h / 4;
     MsmSeg segc[4] = {{dsc, Go + q, q, 0}, {dsc + q, Ho, q, 0}, {dsc + 2 * (size_t)q, Go, q, 1}, {dsc + 3 * (size_t)q, Ho + q, q, 1}};

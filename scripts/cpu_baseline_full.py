@@ -19,6 +19,14 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
 
 
 def main():
+    import threading
+    t_start = time.perf_counter()
+
+    def beat():   # a progress line a minute: the oracle call is silent for minutes
+        while True:
+            time.sleep(60)
+            print("cpu_baseline_full: running, %.0f s" % (time.perf_counter() - t_start), file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     import oracle as O
     import workloads as W
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 5

@@ -1,0 +1,57 @@
+"""Process-level behaviour of the device context:
+
+* the on-disk generator cache (bpg_gens_cache_dir): the first process
+  derives and writes it, the next one loads it and proves the same bytes; a
+  corrupted file is detected and re-derived;
+* two circuit sizes proved concurrently from two host threads on a fresh
+  context (the larger circuit grows the generator set while the smaller
+  circuit's proofs hold their snapshot) give the same bytes as sequential
+  proving.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "robust_worker.py")
+
+
+@pytest.fixture(scope="module")
+def bpg():
+    import workloads
+    return workloads._bpg()
+
+
+def run(*args):
+    r = subprocess.run([sys.executable, WORKER] + list(args), capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_generator_disk_cache(tmp_path):
+    a = run("cache", str(tmp_path))
+    assert not a["gens_from_cache"]
+    files = list(tmp_path.glob("bpg_gens_*.bin"))
+    assert len(files) == 1
+    b = run("cache", str(tmp_path))
+    assert b["gens_from_cache"] and b["proof"] == a["proof"]
+    raw = bytearray(files[0].read_bytes())
+    raw[100000] ^= 1
+    files[0].write_bytes(bytes(raw))
+    c = run("cache", str(tmp_path))                 # checksum mismatch: derived again
+    assert not c["gens_from_cache"] and c["proof"] == a["proof"]
+
+
+def test_concurrent_circuit_sizes(bpg):
+    import workloads as W
+    conc = run("concurrent")
+    ctx = bpg.Context(0)
+    for k, stmt, reps in (("small", W.config2(), 6), ("large", W.config3(), 2)):
+        bpg.set_seed(9)
+        syn = bpg.Synth(*stmt)
+        want = [ctx.r1cs_prove(b"conc", syn.view, bytes([r]) * 32)[0].hex() for r in range(reps)]
+        assert conc[k] == want, k
