@@ -22,7 +22,7 @@ int main(int argc, char **argv) {
     BPG_HIP(hipMalloc(&Go, (size_t)h1 * sizeof(PtD))); BPG_HIP(hipMalloc(&Ho, (size_t)h1 * sizeof(PtD)));
     launch_gens_map(duni, G, N, 0);
     void *tab;
-    const size_t tbytes = (size_t)ntab * 512 * 96;
+    const size_t tbytes = (size_t)ntab * COMB_WIN * COMB_ENT * 96;
     BPG_HIP(hipMalloc(&tab, tbytes));
     hipEvent_t e0, e1; BPG_HIP(hipEventCreate(&e0)); BPG_HIP(hipEventCreate(&e1));
     BPG_HIP(hipDeviceSynchronize());
@@ -41,7 +41,7 @@ int main(int argc, char **argv) {
     CombArgs C{};
     C.gens[0] = G; C.gens[1] = G; C.tab[0] = tab; C.tab[1] = tab; C.out[0] = Go; C.out[1] = Ho;
     C.h1 = h1; C.ntab = ntab; C.nrange = 2; C.rstart[0] = 0; C.rstart[1] = h1 / 3;
-    for (int v = 0; v < 2; v++) for (int r = 0; r < 2; r++) for (int t = 0; t < 3; t++) bpg::radix16_digits(co[v][r][t], C.dig[v][r][t]);
+    for (int v = 0; v < 2; v++) for (int r = 0; r < 2; r++) for (int t = 0; t < 3; t++) { uint8_t sb[32]; co[v][r][t].reduced().to_bytes(sb); comb_digits(sb, C.dig[v][r][t]); }
     ArgStage stage;
     hipStream_t st; BPG_HIP(hipStreamCreate(&st));
     launch_ipp_comb_fold(C, stage, st);

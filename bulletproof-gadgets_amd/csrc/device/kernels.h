@@ -162,9 +162,21 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
                             hipStream_t st);
 // Two-round table fold: G2_i = G_i + c1 G_{i+h1} + c2 G_{i+2h1} + c3 G_{i+3h1}
 // from comb tables of the level-0 generators j in [h1, 4h1) (likewise H).
-// Table entry (w, d) of table index jj = (d+1) 16^w P_{h1+jj}, packed affine
-// Niels, 96 B, at byte offset ((w*8+d)*ntab + jj)*96.
+// Table entry (w, d) of table index jj = (d+1) 2^(COMB_BITS w) P_{h1+jj},
+// packed affine Niels, 96 B, at byte offset ((w*COMB_ENT+d)*ntab + jj)*96.
 #define COMB_MAXRANGE 8
+// Comb radix 2^COMB_BITS: signed digits in [-COMB_ENT, COMB_ENT), so a
+// window keeps the COMB_ENT multiples 1..COMB_ENT of its power; COMB_WIN
+// windows cover a canonical scalar (< 2^253) with its final carry.
+#ifndef COMB_BITS
+#define COMB_BITS 5
+#endif
+#define COMB_ENT (1 << (COMB_BITS - 1))
+#define COMB_WIN ((253 + COMB_BITS) / COMB_BITS)
+static_assert(COMB_WIN <= 64, "comb windows");
+// signed radix-2^COMB_BITS digits of a canonical scalar (32 LE bytes), e[64]
+// zero-filled past COMB_WIN
+void comb_digits(const uint8_t s[32], int8_t e[64]);
 struct CombArgs {
     const void *gens[2];       // G, H (NielsD), level 0
     const void *tab[2];        // comb tables of G, H over [h1, 4 h1)
@@ -172,7 +184,7 @@ struct CombArgs {
     uint32_t h1, ntab;         // ntab = 3 h1
     uint32_t nrange;           // lanes [rstart[r], rstart[r+1]) share digits
     uint32_t rstart[COMB_MAXRANGE];
-    int8_t dig[2][COMB_MAXRANGE][3][64];   // signed radix-16 digits of c1, c2, c3
+    int8_t dig[2][COMB_MAXRANGE][3][64];   // comb_digits of c1, c2, c3
 };
 void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab, hipStream_t st);
 void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st);

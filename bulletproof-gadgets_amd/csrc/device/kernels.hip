@@ -1539,10 +1539,28 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
 
 // ---------------------------------------------------------------------------
 // Comb tables and the two-round table fold (DESIGN.md "IPP rounds 0-1").
-// For generator j = j0 + jj (jj < ntab): entry (w, d) = (d+1) 16^w P_j for
-// w < 64, d < 8, packed affine Niels (96 B) at 16-byte unit
-// ((w*8 + d) * ntab + jj) * 6 — entry-major, so lanes that read the same
-// entry of consecutive generators read one contiguous span.
+// For generator j = j0 + jj (jj < ntab): entry (w, d) = (d+1) R^w P_j,
+// R = 2^COMB_BITS, for w < COMB_WIN, d < COMB_ENT, packed affine Niels (96 B)
+// at 16-byte unit ((w*COMB_ENT + d) * ntab + jj) * 6 — entry-major, so lanes
+// that read the same entry of consecutive generators read one contiguous span.
+void comb_digits(const uint8_t s[32], int8_t e[64]) {
+    int v[64] = {0};
+    for (int i = 0; i < COMB_WIN; i++) {
+        const int bit = COMB_BITS * i;
+        uint32_t x = 0;
+        for (int b = 0; b < COMB_BITS; b++) {
+            const int p = bit + b;
+            if (p < 256) x |= (uint32_t)((s[p >> 3] >> (p & 7)) & 1) << b;
+        }
+        v[i] = (int)x;
+    }
+    for (int i = 0; i + 1 < COMB_WIN; i++) {   // recentre into [-COMB_ENT, COMB_ENT)
+        const int c = (v[i] + COMB_ENT) >> COMB_BITS;
+        v[i] -= c << COMB_BITS;
+        v[i + 1] += c;
+    }
+    for (int i = 0; i < 64; i++) e[i] = (int8_t)(i < COMB_WIN ? v[i] : 0);
+}
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_comb_build(const gen *__restrict__ gens, uint32_t j0, uint32_t ntab,
                                                    uint4 *__restrict__ tab) {
@@ -1554,17 +1572,17 @@ __global__ __launch_bounds__(64) void k_comb_build(const gen *__restrict__ gens,
     gen_to_cached(c, g);
     ge pw;
     ge_from_cached(pw, c);
-    for (int w = 0; w < 64; w++) {
+    for (int w = 0; w < COMB_WIN; w++) {
         gec pc;
         ge_to_cached(pc, pw);
         ge q = pw;
-        for (int d = 0; d < 8; d++) {
+        for (int d = 0; d < COMB_ENT; d++) {
             if (d) ge_add_c(q, q, pc);
             gen e;
             ge_to_niels(e, q);
-            genp_store(tab + ((size_t)(w * 8 + d) * ntab + jj) * 6, e);
+            genp_store(tab + ((size_t)(w * COMB_ENT + d) * ntab + jj) * 6, e);
         }
-        ge_dbl(pw, q);   // 16^(w+1) P
+        ge_dbl(pw, q);   // R^(w+1) P = 2 (COMB_ENT R^w P)
     }
 }
 void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab, hipStream_t st) {
@@ -1576,8 +1594,8 @@ void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab
 
 // Output lane i < h1 of vector v (0 = G, 1 = H):
 //   out_i = P_i + sum_{t<3} c_t * P_{i + (t+1) h1}
-// with per-lane-range coefficient digits (signed radix 16, LSB first); no
-// doublings: every nonzero digit is one table read and one 7M madd.
+// with per-lane-range coefficient digits (signed radix 2^COMB_BITS, LSB
+// first); no doublings: every nonzero digit is one table read and one 7M madd.
 __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restrict__ Ap) {
     const CombArgs &A = *Ap;
     const uint32_t nb = (A.h1 + 63) / 64;
@@ -1598,7 +1616,7 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
     for (int t = 0; t < 3; t++) {
         const uint32_t jj = i + (uint32_t)t * A.h1;
         const uint32_t *dw = reinterpret_cast<const uint32_t *>(A.dig[v][r][t]);
-        for (int w4 = 0; w4 < 16; w4++) {
+        for (int w4 = 0; w4 < (COMB_WIN + 3) / 4; w4++) {
             const uint32_t packed = dw[w4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1606,7 +1624,7 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
                 if (d == 0) continue;
                 const int w = 4 * w4 + k;
                 const int m = d < 0 ? -d : d;
-                const uint4 *e = tab + ((size_t)(w * 8 + m - 1) * A.ntab + jj) * 6;
+                const uint4 *e = tab + ((size_t)(w * COMB_ENT + m - 1) * A.ntab + jj) * 6;
                 uint4 q[6];
 #pragma unroll
                 for (int u = 0; u < 6; u++) q[u] = e[u];

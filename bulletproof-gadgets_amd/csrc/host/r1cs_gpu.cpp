@@ -224,7 +224,7 @@ std::shared_ptr<CombTables> DeviceContext::comb(const std::shared_ptr<const GenS
     if (it != combs.end()) return it->second;
     const double t0 = now_ms();
     const uint32_t h1 = N / 4, ntab = 3 * h1;
-    const size_t bytes = (size_t)ntab * 512 * 96;   // per vector
+    const size_t bytes = (size_t)ntab * COMB_WIN * COMB_ENT * 96;   // per vector
     BPG_HIP(hipSetDevice(device));
     size_t free_b = 0, total_b = 0;
     BPG_HIP(hipMemGetInfo(&free_b, &total_b));
@@ -1050,9 +1050,11 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                         const Scalar c2 = rho_p[2 * v + (b0 ? 1 : 0)];
                         const Scalar c3 = c1 * rho_p[2 * v + (b0h ? 1 : 0)];
                         if (table) {
-                            radix16_digits(c1, C.dig[v][r][0]);
-                            radix16_digits(c2, C.dig[v][r][1]);
-                            radix16_digits(c3, C.dig[v][r][2]);
+                            uint8_t sb[3][32];
+                            c1.reduced().to_bytes(sb[0]); c2.reduced().to_bytes(sb[1]); c3.reduced().to_bytes(sb[2]);
+                            comb_digits(sb[0], C.dig[v][r][0]);
+                            comb_digits(sb[1], C.dig[v][r][1]);
+                            comb_digits(sb[2], C.dig[v][r][2]);
                         } else {
                             coef[v][r][0] = to_dev(c1); coef[v][r][1] = to_dev(c2); coef[v][r][2] = to_dev(c3);
                         }

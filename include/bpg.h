@@ -136,7 +136,7 @@ void bpg_ctx_destroy(bpg_ctx *ctx);
 /* IPP fold strategy of the calls made through `ctx` (bpg_r1cs_prove,
  * bpg_prepare; a prepared circuit keeps the strategy it was prepared with).
  * Proof bytes are identical under every strategy.
- *   fold_tables 1: comb tables of the generators (HBM-resident, ~74 KB x N
+ *   fold_tables 1: comb tables of the generators (HBM-resident, ~117 KB x N
  *     per device) fold IPP rounds 0-1 in one table pass; 0: per-round
  *     variable-base fold; -1 (default): on unless env BPG_FOLD_TABLES=0
  *     (tables are skipped when they do not fit in free HBM).
