@@ -62,9 +62,10 @@ def parse():
 
 
 # single kernels bracketed live (bpg name -> rocprofv3 kernel name)
-KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1>", "msm_pass1_affine": "k_rbk_pass<true, 2>", "msm_pass1_cached": "k_rbk_pass<true, 0>",
+KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1, true>", "msm_pass1_cached": "k_rbk_pass<true, 0, false>",
            "ipp_fold_points": "k_ipp_fold_points<gec>",
-           "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "flatten": "k_flatten_short"}
+           "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "ipp_fold3": "k_ipp_fold3<gec>",
+           "flatten": "k_flatten_short"}
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 FEMUL_PEAK_G = 261.5         # GF(2^255-19) multiplies/s x1e9, measured: profiles/r02d_valu_micro.log (fe_variants V2)
 

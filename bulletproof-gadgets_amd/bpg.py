@@ -28,7 +28,7 @@ EXPORTS = [
     "bpg_mimc_sponge", "bpg_profile_enable", "bpg_kernel_stats", "bpg_kernel_stats_reset", "bpg_rng_selftest",
     "bpg_rng_rate", "bpg_r1cs_verify_shard", "bpg_point_sum", "bpg_kernel_femul",
     "bpg_verify_batch", "bpg_prepare_verifier", "bpg_gens_cache_dir", "bpg_ctx_set_fold_tables",
-    "bpg_ctx_set_fold_pairs", "bpg_ctx_setup_stats", "bpg_r1cs_prove_sharded", "bpg_cs_create", "bpg_cs_free",
+    "bpg_ctx_set_fold_pairs", "bpg_ctx_set_ipp_tail", "bpg_ctx_setup_stats", "bpg_r1cs_prove_sharded", "bpg_cs_create", "bpg_cs_free",
     "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
     "bpg_prove_prepared",
@@ -91,6 +91,7 @@ def lib():
         L.bpg_gens_cache_dir.argtypes = [cp]
         L.bpg_ctx_set_fold_tables.argtypes = [vp, ctypes.c_int]
         L.bpg_ctx_set_fold_pairs.argtypes = [vp, ctypes.c_int]
+        L.bpg_ctx_set_ipp_tail.argtypes = [vp, ctypes.c_int]
         L.bpg_ctx_setup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_r1cs_prove_sharded.argtypes = [vp, vp, sz, vp, vp, u32, u32, ALLGATHER_FN, vp, vp, sz,
                                              ctypes.POINTER(sz), vp]
@@ -330,10 +331,12 @@ class Context:
         if not self.h:
             raise BpgError(last_error())
 
-    def set_strategy(self, fold_tables=-1, fold_pairs=-1):
-        """IPP fold strategy of this context's calls (bpg_ctx_set_fold_*)."""
+    def set_strategy(self, fold_tables=-1, fold_pairs=-1, ipp_tail=-1):
+        """IPP fold strategy of this context's calls (bpg_ctx_set_fold_*,
+        bpg_ctx_set_ipp_tail); fold_pairs 2 folds rounds in triples."""
         if lib().bpg_ctx_set_fold_tables(self.h, fold_tables) != 0 or \
-                lib().bpg_ctx_set_fold_pairs(self.h, fold_pairs) != 0:
+                lib().bpg_ctx_set_fold_pairs(self.h, fold_pairs) != 0 or \
+                lib().bpg_ctx_set_ipp_tail(self.h, ipp_tail) != 0:
             raise BpgError("bad strategy")
 
     def setup_stats(self):

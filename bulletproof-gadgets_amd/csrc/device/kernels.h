@@ -50,6 +50,8 @@ ProfSink *prof_sink();
 // Generators and decompressed inputs live in HBM as affine Niels points
 // (128 B, one line per random gather); folded generators are cached points
 // (160 B); MSM window rows returned to the host are extended.
+// out[i] = -in[i] (affine Niels: swap y+x / y-x, negate 2dxy)
+void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = from_uniform_bytes(uniform[64*i .. 64*i+64))
 void launch_gens_map(const uint8_t *uniform, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = v[i]*B + vb[i]*B_blinding using fixed-base tables (64 x 8 points each)
@@ -60,13 +62,18 @@ void launch_compress(const NielsD *in, uint32_t *out, uint32_t count, hipStream_
 void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count, hipStream_t st);
 
 // -------------------------------------------------------------- MSM
+#define MSM_MAX_SEGS 18   // segments per MSM job (a round-triple IPP job: 2 x (8 + 1))
 #define MSM_CACHED 0   // bases are cached points (PtD)
 #define MSM_NIELS 1    // bases are affine Niels points (NielsD)
 struct MsmSeg {
     const ScD *scal;   // canonical scalars (< l)
     const void *base;  // PtD (cached) or NielsD, per the job's format
-    uint32_t count;
+    uint32_t count;    // < 2^26
     uint32_t msm;      // which MSM of the job this segment contributes to
+    // points from base + negofs on are the negatives of the segment's points
+    // (0: no such copy). When every segment of a Niels job has one, a
+    // negative digit gathers the negated base instead of negating it.
+    int64_t negofs = 0;
 };
 struct MsmPlan {
     int c, W, nmsm, rows, half;   // W: digit windows per scalar = rows per MSM
@@ -169,7 +176,7 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
 // window keeps the COMB_ENT multiples 1..COMB_ENT of its power; COMB_WIN
 // windows cover a canonical scalar (< 2^253) with its final carry.
 #ifndef COMB_BITS
-#define COMB_BITS 5
+#define COMB_BITS 6
 #endif
 #define COMB_ENT (1 << (COMB_BITS - 1))
 #define COMB_WIN ((253 + COMB_BITS) / COMB_BITS)
@@ -204,6 +211,23 @@ struct LazyArgs {
 // msm_scal[0..8h) (layout in kernels.hip), c_L -> [8h], c_R -> [8h+1]
 void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
                           ScD *msm_scal, ScD *partial, hipStream_t st);
+// Round k+2 of a round triple (levels k+1, k+2 unmaterialised): each base
+// expanded into four level-k points. r1/r0: rounds k+1 / k fold scalars
+// (Montgomery) per vector (0 = G, 1 = H) and class (1: the pair straddles n).
+struct Deep2Args {
+    ScD r1[2][2], r0[2][2];
+};
+// msm_scal[0..16h) (layout in kernels.hip), c_L -> [16h], c_R -> [16h+1]
+void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
+                           ScD *msm_scal, ScD *partial, hipStream_t st);
+// Three-round Straus fold from level k (NielsD at level 0, else PtD):
+// out_i = P_i + sum_{t=1..7} c_t P_{i + t hq}, i < hq; coef[v][r][t-1] canonical
+// for lanes [rstart[r], rstart[r+1]). `tab`: odd-multiple tables,
+// ipp_fold3_table_bytes(hq, nrange) bytes.
+size_t ipp_fold3_table_bytes(uint32_t hq, uint32_t nrange);
+void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq, uint32_t nrange,
+                      const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][7], PtD *Gout, PtD *Hout,
+                      void *tab, size_t tab_bytes, ArgStage &stage, hipStream_t st);
 // IPP tail (DESIGN.md "IPP tail without folds"): below a few thousand lanes
 // the generators stay at the last materialised level (M points each) with a
 // per-point weight w_j (Montgomery form), so the round-k base i is

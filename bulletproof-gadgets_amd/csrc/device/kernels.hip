@@ -200,15 +200,20 @@ void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count,
 #define RBK_BLOCK 256
 #endif
 #define RBK_CHUNK (RBK_T * RBK_BLOCK)
-#define MSM_MAXSEG 12
+#define MSM_MAXSEG MSM_MAX_SEGS
 struct SegTab {
     const sc *scal[MSM_MAXSEG];
     const void *base[MSM_MAXSEG];
+    const void *neg[MSM_MAXSEG];    // negated copies (NEGC jobs), else = base
     uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t row0[MSM_MAXSEG];
     int n;
 };
-#define MSM_VAL_G 0x7fffffffu       // val = sign << 31 | point
+// val = sign << 31 | segment << 26 | point index within the segment: the
+// digit kernel resolves the segment once per point, so the run reduction
+// gathers from a per-block pointer table in LDS without searching segments
+#define MSM_SEG_SHIFT 26
+#define MSM_LOC_MASK ((1u << MSM_SEG_SHIFT) - 1)
 DEVI int seg_of(const SegTab &T, uint32_t g) {
     int si = 0;
 #pragma unroll
@@ -231,6 +236,7 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
     sc_load(k, T.scal[si] + (g - T.gofs[si]));
     uint32_t carry = 0, mask = (1u << c) - 1, full = 1u << c;
     const uint32_t m = T.row0[si];
+    const uint32_t loc = (uint32_t)si << MSM_SEG_SHIFT | (g - T.gofs[si]);
     for (int w = 0; w < W; w++) {
         int bit = w * c;
         int lo = bit >> 5, sh = bit & 31;
@@ -239,7 +245,7 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
         uint32_t d = (uint32_t)(x >> sh) & mask;
         d += carry;
         const uint32_t row = (uint32_t)w * nmsm + m;
-        uint32_t slot = half, val = g;
+        uint32_t slot = half, val = loc;
         if (d > half) {
             uint32_t mag = full - d;
             carry = 1;
@@ -430,23 +436,55 @@ DEVI void rbk_stage(uint32_t *sk, const uint32_t *__restrict__ keys, uint64_t ba
     }
 }
 // Base gathers by the job's base format: cached (160 B) or affine Niels
-// (128 B, one line, 7M madd).
+// (128 B, one line, 7M madd). The block's segment pointers sit in LDS:
+// sptr[seg] the bases, sptr[MSM_MAXSEG + seg] their negated copies (NEGC) —
+// a negative digit then gathers -P and adds it as is.
 template <int FMT> struct BaseOf { typedef gec T; };
 template <> struct BaseOf<MSM_NIELS> { typedef gen T; };
-template <int FMT>
-DEVI void msm_load_base(typename BaseOf<FMT>::T &p, const SegTab &T, uint32_t v) {
-    const uint32_t g = v & MSM_VAL_G;
-    const int si = seg_of(T, g);
-    pt_load(p, reinterpret_cast<const typename BaseOf<FMT>::T *>(T.base[si]) + (g - T.gofs[si]));
+// pt_load from a pointer known to be global memory (the LDS table hides the
+// address space; a generic pointer would compile to flat loads)
+template <class P>
+DEVI void pt_load_global(P &p, uint64_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(1))) const uint4 g4;
+#else
+    typedef const uint4 g4;   // host pass: the function is never called there
+#endif
+    constexpr int NQ = sizeof(P) / 16;
+    const g4 *s = reinterpret_cast<const g4 *>(addr);
+    uint32_t *d = reinterpret_cast<uint32_t *>(&p);
+#pragma unroll
+    for (int i = 0; i < NQ; i++) { const uint4 q = s[i]; d[4 * i] = q.x; d[4 * i + 1] = q.y; d[4 * i + 2] = q.z; d[4 * i + 3] = q.w; }
 }
-DEVI void msm_add_loaded(ge &acc, gen &p, bool neg) { gen_cneg(p, neg); ge_madd(acc, acc, p); }
-DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) { gec_cneg(p, neg); ge_add_c(acc, acc, p); }
+template <int FMT, bool NEGC>
+DEVI void msm_load_base(typename BaseOf<FMT>::T &p, const uint64_t *sptr, uint32_t v) {
+    const uint32_t si = (v >> MSM_SEG_SHIFT) & 31u;
+    const uint32_t sel = NEGC ? (v >> 31) * MSM_MAXSEG + si : si;
+    pt_load_global(p, sptr[sel] + (uint64_t)(v & MSM_LOC_MASK) * sizeof(typename BaseOf<FMT>::T));
+}
+template <bool NEGC> DEVI void msm_add_loaded(ge &acc, gen &p, bool neg) {
+    if (!NEGC) gen_cneg(p, neg);
+    ge_madd(acc, acc, p);
+}
+template <bool NEGC> DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) {
+    if (!NEGC) gec_cneg(p, neg);
+    ge_add_c(acc, acc, p);
+}
 
 // FIRST: entries are (key, signed base index) and the gather of entry i+1 is
-// issued before entry i's addition; otherwise entries are slots (key or
-// key|RBK_FILL, extended point at the same index) of the previous pass.
-template <bool FIRST, int FMT>
-__global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restrict__ keys,
+// issued before entry i's addition (two base registers used in turn, so no
+// copy between them); otherwise entries are slots (key or key|RBK_FILL,
+// extended point at the same index) of the previous pass.
+// RBK_PINGPONG: entry i+1's base is gathered into the other of two base
+// registers (no copy, more VGPRs); else into the one just consumed.
+#ifndef RBK_PINGPONG
+#define RBK_PINGPONG 0
+#endif
+#ifndef RBK_WAVES
+#define RBK_WAVES (RBK_PINGPONG ? 2 : 3)   // waves per SIMD the run reduction is compiled for
+#endif
+template <bool FIRST, int FMT, bool NEGC>
+__global__ __launch_bounds__(RBK_BLOCK, (FIRST && FMT == MSM_CACHED) ? 2 : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         const ge *__restrict__ pin, SegTab T, uint64_t E,
                                                         uint32_t invalid, int cw, uint32_t *__restrict__ kout,
@@ -454,6 +492,7 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restri
                                                         uint8_t *__restrict__ bflag) {
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
     __shared__ uint32_t sv[FIRST ? RBK_CHUNK + RBK_BLOCK : 1];
+    __shared__ uint64_t sptr[FIRST ? 2 * MSM_MAXSEG : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * RBK_CHUNK;
     rbk_stage(sk, keys, base, E, invalid);
@@ -461,6 +500,10 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restri
         for (uint32_t k = t; k < RBK_CHUNK; k += RBK_BLOCK) {
             uint64_t idx = base + k;
             sv[rbk_lds(k)] = idx < E ? vals[idx] : 0;
+        }
+        if (t < MSM_MAXSEG) {
+            sptr[t] = reinterpret_cast<uint64_t>(T.base[t]);
+            sptr[MSM_MAXSEG + t] = reinterpret_cast<uint64_t>(T.neg[t]);
         }
     }
     __syncthreads();
@@ -478,40 +521,63 @@ __global__ __launch_bounds__(RBK_BLOCK) void k_rbk_pass(const uint32_t *__restri
     uint32_t cur = first;
     ge acc;
     ge_identity(acc);
-    typename BaseOf<FMT>::T pnext;
-    if (FIRST && !rbk_trash(first, cw)) msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T)]);
-    for (uint32_t i = 0; i < RBK_T; i++) {
-        const uint32_t x = sk[rbk_lds(t * RBK_T + i)];
-        const uint32_t k = RBK_KEY(x);
-        if (k == invalid) break;
-        if (k != cur) {
-            if (!head_done) {
-                if (open_start) { ko[0] = cur | (real ? 0u : RBK_FILL); if (real) ge_store(po, acc); }
-                else { if (real) { ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1; } ko[0] = cur | RBK_FILL; }
-                head_done = true;
-            } else if (real) {
-                ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1;
-            }
-            cur = k; real = false;
-            ge_identity(acc);
+    // a new key closes the current run: the head piece goes to the next pass
+    // (or its bucket when the run began in this chunk), later runs to buckets
+    auto close_run = [&](uint32_t k) {
+        if (!head_done) {
+            if (open_start) { ko[0] = cur | (real ? 0u : RBK_FILL); if (real) ge_store(po, acc); }
+            else { if (real) { ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1; } ko[0] = cur | RBK_FILL; }
+            head_done = true;
+        } else if (real) {
+            ge_store(buckets + rbk_bucket(cur, cw), acc); bflag[rbk_bucket(cur, cw)] = 1;
         }
-        if (FIRST) {
-            // the base of entry i + 1 is in flight while entry i is added;
-            // zero digits (trash, sorted to the end of their row) are never added
-            const bool trash = rbk_trash(k, cw);
-            typename BaseOf<FMT>::T p = pnext;
-            const uint32_t v = sv[rbk_lds(t * RBK_T + i)];
+        cur = k; real = false;
+        ge_identity(acc);
+    };
+    if constexpr (FIRST) {
+        typedef typename BaseOf<FMT>::T BT;
+        BT pa, pb;
+        const uint32_t *skt = sk + rbk_lds(t * RBK_T), *svt = sv + rbk_lds(t * RBK_T);   // chunk has no pad inside
+        if (!rbk_trash(first, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[0]);
+        // entry i: its base is in `use`; entry i+1's gather goes to `fill`.
+        // Returns false at the chunk's end (padding key).
+        auto step = [&](uint32_t i, BT &use, BT &fill) -> bool {
+            const uint32_t k = RBK_KEY(skt[i]);
+            if (k == invalid) return false;
+            if (k != cur) close_run(k);
+            const uint32_t v = svt[i];
             if (i + 1 < RBK_T) {
-                const uint32_t kn = RBK_KEY(sk[rbk_lds(t * RBK_T + i + 1)]);
-                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT>(pnext, T, sv[rbk_lds(t * RBK_T + i + 1)]);
+                const uint32_t kn = RBK_KEY(skt[i + 1]);
+                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(fill, sptr, svt[i + 1]);
             }
-            if (trash) continue;
-            msm_add_loaded(acc, p, v >> 31);
-            real = true;
-        } else if (!(x & RBK_FILL)) {
-            ge p; ge_load(p, pin + gs + i);
-            ge_add(acc, acc, p);
-            real = true;
+            // zero digits (trash, sorted to the end of their row) are never added
+            if (!rbk_trash(k, cw)) { msm_add_loaded<NEGC>(acc, use, v >> 31); real = true; }
+            return true;
+        };
+#if RBK_PINGPONG
+        static_assert(RBK_T % 2 == 0, "chunk of an even number of entries");
+        for (uint32_t i = 0; i < RBK_T; i += 2) {
+            if (!step(i, pa, pb)) break;
+            if (!step(i + 1, pb, pa)) break;
+        }
+#else
+        for (uint32_t i = 0; i < RBK_T; i++) {
+            BT use = pa;
+            if (!step(i, use, pa)) break;
+        }
+        (void)pb;
+#endif
+    } else {
+        for (uint32_t i = 0; i < RBK_T; i++) {
+            const uint32_t x = sk[rbk_lds(t * RBK_T + i)];
+            const uint32_t k = RBK_KEY(x);
+            if (k == invalid) break;
+            if (k != cur) close_run(k);
+            if (!(x & RBK_FILL)) {
+                ge p; ge_load(p, pin + gs + i);
+                ge_add(acc, acc, p);
+                real = true;
+            }
         }
     }
     const bool tail_open = nk == cur;
@@ -716,7 +782,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         T.gofs[i] = (uint32_t)total;
         total += segs[i].count;
     }
-    if (total > MSM_VAL_G) throw HipError(hipErrorInvalidValue, "msm job too large", __FILE__, __LINE__);
+    if (total > 0x7fffffffu) throw HipError(hipErrorInvalidValue, "msm job too large", __FILE__, __LINE__);
     T.gofs[nseg] = (uint32_t)total;
     p.total = total;
     p.c = msm_window(total);
@@ -735,9 +801,16 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         if (!mtot[m]) moff[m] = T.gofs[i];
         mtot[m] += segs[i].count;
     }
+    // negated copies: used when every segment of a Niels job has one
+    bool negc = fmt == MSM_NIELS;
+    const size_t psz = fmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
     for (int i = 0; i < nseg; i++) {
+        if (segs[i].count > MSM_LOC_MASK) throw HipError(hipErrorInvalidValue, "msm segment too large", __FILE__, __LINE__);
         T.scal[i] = AS_CSC(segs[i].scal);
         T.base[i] = segs[i].base;
+        T.neg[i] = segs[i].negofs ? (const void *)((const uint8_t *)segs[i].base + segs[i].negofs * (int64_t)psz)
+                                  : segs[i].base;
+        negc = negc && segs[i].negofs != 0;
         T.row0[i] = segs[i].msm;
     }
     p.E0 = (uint64_t)p.W * total;
@@ -805,15 +878,18 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"),
                      96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels
                      (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);
-        if (p.passes == 0 && fmt == MSM_NIELS)
-            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin, T,
-                               E, invalid, p.c, kout, pout, buckets, bflag);
+        if (p.passes == 0 && fmt == MSM_NIELS && negc)
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, true>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+                               pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
+        else if (p.passes == 0 && fmt == MSM_NIELS)
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, false>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+                               pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         else if (p.passes == 0)
-            hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
-                               T, E, invalid, p.c, kout, pout, buckets, bflag);
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED, false>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+                               pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         else
-            hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals, pin,
-                               T, E, invalid, p.c, kout, pout, buckets, bflag);
+            hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED, false>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
+                               vals, pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
         p.passes++;
         E = 2 * (uint64_t)nblocks * RBK_BLOCK;
@@ -1538,6 +1614,188 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
 }
 
 // ---------------------------------------------------------------------------
+// Three-round Straus fold (DESIGN.md "IPP fold in round triples"): lane i of
+// level k+3 is sum_{t<8} c_t P_{i + t hq} over the level-k points (c_0 = 1):
+// seven scalar multiples sharing one chain of ~252 doublings. The odd
+// multiples P, 3P (WN = 3) or P..7P (WN = 4) of the seven points sit in a
+// per-block global table, word-major (lane-contiguous, so every table read
+// is coalesced); the next op's entry is loaded before the doublings.
+// ---------------------------------------------------------------------------
+#ifndef BPG_FOLD3_WNAF
+#define BPG_FOLD3_WNAF 4
+#endif
+#define FOLDN_MAXSEG (2 * COMB_MAXRANGE)
+#define FOLDN_MAXOPS 640
+#define FOLDN_K 7
+#define FOLDN_MULT (1 << (BPG_FOLD3_WNAF - 2))        // odd multiples per point
+#define FOLDN_TABW (FOLDN_K * FOLDN_MULT * 40 * 64)   // table words per block
+struct FoldNArgs {
+    const void *in[2];
+    gec *out[2];
+    uint32_t *tab;             // blocks x FOLDN_TABW words
+    uint32_t hq, nseg;
+    uint32_t start[FOLDN_MAXSEG], end[FOLDN_MAXSEG], blk0[FOLDN_MAXSEG + 1], vec[FOLDN_MAXSEG];
+    uint32_t nops[FOLDN_MAXSEG], tail[FOLDN_MAXSEG];
+    // op: gap (8 bits) | point t - 1 << 8 (3 bits) | (m >> 1) << 11 (2 bits) | neg << 15
+    uint16_t ops[FOLDN_MAXSEG][FOLDN_MAXOPS];
+};
+DEVI void foldn_put(uint32_t *tb, const gec &c) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&c);
+#pragma unroll
+    for (int k = 0; k < 40; k++) tb[k * 64] = w[k];
+}
+DEVI void foldn_get(gec &c, const uint32_t *tb) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(&c);
+#pragma unroll
+    for (int k = 0; k < 40; k++) w[k] = tb[k * 64];
+}
+template <class P>
+__global__ __launch_bounds__(64, 1) void k_ipp_fold3(const FoldNArgs *__restrict__ Ap) {
+    const FoldNArgs &A = *Ap;
+    uint32_t b = blockIdx.x, sg = 0;
+    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
+    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
+    if (i >= A.end[sg]) return;
+    const uint32_t v = A.vec[sg], nops = A.nops[sg];
+    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
+    const uint16_t *ops = A.ops[sg];
+    const uint32_t hq = A.hq;
+    gec P0;
+    if (nops == 0) {
+        load_as_cached(P0, Pin + i);
+        gec_store(A.out[v] + i, P0);
+        return;
+    }
+    uint32_t *tb = A.tab + (size_t)b * FOLDN_TABW + threadIdx.x;
+    for (int t = 0; t < FOLDN_K; t++) {
+        gec c1;
+        load_as_cached(c1, Pin + (size_t)(t + 1) * hq + i);
+        foldn_put(tb + (t * FOLDN_MULT) * 40 * 64, c1);
+        ge pr, p2, q;
+        fe_sub(pr.X, c1.YpX, c1.YmX);   // projective (2X : 2Y : 2Z), enough to double
+        fe_add(pr.Y, c1.YpX, c1.YmX);
+        pr.Z = c1.Z2;
+        ge_dbl(p2, pr);
+        ge_add_c(q, p2, c1);             // 3P
+        gec c;
+        ge_to_cached(c, q);
+        foldn_put(tb + (t * FOLDN_MULT + 1) * 40 * 64, c);
+        if constexpr (FOLDN_MULT > 2) {
+            gec d2;
+            ge_to_cached(d2, p2);
+            for (int m = 2; m < FOLDN_MULT; m++) {   // (2m+1)P = (2m-1)P + 2P
+                ge_add_c(q, q, d2);
+                ge_to_cached(c, q);
+                foldn_put(tb + (t * FOLDN_MULT + m) * 40 * 64, c);
+            }
+        }
+    }
+    auto entry = [&](uint32_t op) { return tb + (((op >> 8) & 7) * FOLDN_MULT + ((op >> 11) & 3)) * 40 * 64; };
+    ge acc;
+    {
+        const uint32_t op = fold2_op(ops, 0);
+        gec c;
+        foldn_get(c, entry(op));
+        if (op >> 15) gec_neg(c, c);
+        ge_from_cached(acc, c);
+    }
+    gec c;
+    if (nops > 1) foldn_get(c, entry(fold2_op(ops, 1)));
+    for (uint32_t k = 1; k < nops; k++) {
+        const uint32_t op = fold2_op(ops, k);
+        const uint32_t g = op & 255;
+        gec cn;
+        if (k + 1 < nops) foldn_get(cn, entry(fold2_op(ops, k + 1)));
+        if (g) {
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+        c = cn;
+    }
+    const uint32_t tail = A.tail[sg];
+    if (tail) {
+        for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
+        ge_dbl_t<true>(acc, acc);
+    }
+    load_as_cached(P0, Pin + i);
+    ge r;
+    ge_add_c(r, acc, P0);
+    gec out;
+    ge_to_cached(out, r);
+    gec_store(A.out[v] + i, out);
+}
+size_t ipp_fold3_table_bytes(uint32_t hq, uint32_t nrange) {
+    // blocks: per vector and range, whole 64-lane blocks
+    return ((size_t)2 * (hq / 64 + nrange + 1)) * FOLDN_TABW * 4;
+}
+void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq, uint32_t nrange,
+                      const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][7], PtD *Gout, PtD *Hout,
+                      void *tab, size_t tab_bytes, ArgStage &stage, hipStream_t st) {
+    if (!hq) return;
+    if (nrange < 1 || nrange > COMB_MAXRANGE) throw HipError(hipErrorInvalidValue, "fold3 ranges", __FILE__, __LINE__);
+    if (!stage.dev) {
+        BPG_HIP(hipMalloc(&stage.dev, sizeof(FoldNArgs)));
+        BPG_HIP(hipHostMalloc(&stage.host, sizeof(FoldNArgs), hipHostMallocDefault));
+        BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
+    } else {
+        event_wait(stage.copied);
+    }
+    FoldNArgs &A = *reinterpret_cast<FoldNArgs *>(stage.host);
+    A.in[0] = Gin; A.in[1] = Hin;
+    A.out[0] = AS_GEC(Gout); A.out[1] = AS_GEC(Hout);
+    A.tab = reinterpret_cast<uint32_t *>(tab);
+    A.hq = hq;
+    A.nseg = 0;
+    uint32_t blocks = 0;
+    double fem = 0;
+    constexpr int WN = BPG_FOLD3_WNAF;
+    for (uint32_t v = 0; v < 2; v++)
+        for (uint32_t r = 0; r < nrange; r++) {
+            const uint32_t lo = rstart[r], hi = r + 1 < nrange ? rstart[r + 1] : hq;
+            if (hi <= lo) continue;
+            const uint32_t s = A.nseg++;
+            A.start[s] = lo; A.end[s] = hi; A.vec[s] = v; A.blk0[s] = blocks;
+            blocks += nblk(hi - lo, 64);
+            int8_t d[FOLDN_K][264];
+            int len[FOLDN_K], top = -1;
+            for (int t = 0; t < FOLDN_K; t++) {
+                len[t] = wnaf_digits(coef[v][r][t], WN, d[t]);
+                top = std::max(top, len[t] - 1);
+            }
+            uint32_t n = 0, dbl = 0;
+            int last = -1;
+            for (int pos = top; pos >= 0; pos--)
+                for (int t = 0; t < FOLDN_K; t++) {
+                    if (pos >= len[t] || !d[t][pos]) continue;
+                    if (n >= FOLDN_MAXOPS) throw HipError(hipErrorInvalidValue, "fold3 ops", __FILE__, __LINE__);
+                    const int dg = d[t][pos], m = dg < 0 ? -dg : dg;
+                    const uint32_t gap = last < 0 ? 0u : (uint32_t)(last - pos);
+                    if (gap > 255) throw HipError(hipErrorInvalidValue, "fold3 gap", __FILE__, __LINE__);
+                    A.ops[s][n++] = (uint16_t)(gap | ((uint32_t)t << 8) | ((uint32_t)(m >> 1) << 11) |
+                                               ((dg < 0 ? 1u : 0u) << 15));
+                    dbl += gap;
+                    last = pos;
+                }
+            A.nops[s] = n;
+            A.tail[s] = last < 0 ? 0u : (uint32_t)last;
+            dbl += A.tail[s];
+            fem += (double)(hi - lo) * (7.0 * dbl + 8.0 * n + FOLDN_K * (7.0 + 9.0 * (FOLDN_MULT - 1)) + 12.0);
+        }
+    A.blk0[A.nseg] = blocks;
+    if (!blocks) return;
+    if ((size_t)blocks * FOLDN_TABW * 4 > tab_bytes) throw HipError(hipErrorInvalidValue, "fold3 table", __FILE__, __LINE__);
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldNArgs), hipMemcpyHostToDevice, st));
+    BPG_HIP(hipEventRecord(stage.copied, st));
+    // reads 8 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
+    ProfScope ps("ipp_fold3", 2.0 * hq * 9 * 64, fem);
+    const FoldNArgs *dA = reinterpret_cast<const FoldNArgs *>(stage.dev);
+    if (in_fmt == MSM_NIELS) hipLaunchKernelGGL(k_ipp_fold3<gen>, dim3(blocks), dim3(64), 0, st, dA);
+    else hipLaunchKernelGGL(k_ipp_fold3<gec>, dim3(blocks), dim3(64), 0, st, dA);
+    BPG_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
 // Comb tables and the two-round table fold (DESIGN.md "IPP rounds 0-1").
 // For generator j = j0 + jj (jj < ntab): entry (w, d) = (d+1) R^w P_j,
 // R = 2^COMB_BITS, for w < COMB_WIN, d < COMB_ENT, packed affine Niels (96 B)
@@ -1716,6 +1974,65 @@ void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppR
 }
 
 // IPP tail round over the materialised level (M points per vector).
+// Round k+2 of a round triple: each level-(k+2) base x (2h of them per
+// vector) expanded into its four level-k points x + 2h t, t < 4, with
+// coefficients (1, r1(x), r0(x), r1(x) r0(x + 2h)), r1 the round-(k+1) fold
+// scalar (class: x < n <= x + 2h), r0 the round-k one (class: y < n <= y + 4h).
+// Layout: family f in [L: G_hi, H_lo | R: G_lo, H_hi], term t:
+// out[(4 f + t) h + i]; c_L -> out[16h], c_R -> out[16h + 1].
+__global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                        const sc *__restrict__ yipm, IppRoundArgs A, Deep2Args Z,
+                                                        sc *__restrict__ out, sc *__restrict__ partial) {
+    sc acc[2];
+    sc_zero(acc[0]); sc_zero(acc[1]);
+    const uint32_t h = A.h, n = A.n;
+    const sc lamG1 = *reinterpret_cast<const sc *>(&A.lamG1), lamGu = *reinterpret_cast<const sc *>(&A.lamGu);
+    const sc muH1 = *reinterpret_cast<const sc *>(&A.muH1), muHu = *reinterpret_cast<const sc *>(&A.muHu);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < h; i += gridDim.x * blockDim.x) {
+        sc aL, aR, bL, bR, t, s, y;
+        sc_load(aL, a + i); sc_load(aR, a + h + i); sc_load(bL, b + i); sc_load(bR, b + h + i);
+        mm(t, aL, bR); sc_add(acc[0], acc[0], t);
+        mm(t, aR, bL); sc_add(acc[1], acc[1], t);
+        const uint32_t lo = i, hi = h + i;
+        const bool lo_real = lo < n, hi_real = hi < n;
+        // family scalar and its level-(k+2) lane x, per family
+#pragma unroll
+        for (int f = 0; f < 4; f++) {
+            const bool G = (f & 1) == 0;          // 0: L G_hi, 1: L H_lo, 2: R G_lo, 3: R H_hi
+            const uint32_t x = (f == 0 || f == 3) ? hi : lo;
+            const bool real = x < n;
+            if (f == 0) mm(s, aL, real ? lamG1 : lamGu);
+            else if (f == 2) mm(s, aR, real ? lamG1 : lamGu);
+            else {
+                sc_load(y, yipm + x);
+                mm(t, f == 1 ? bR : bL, y);
+                mm(s, t, real ? muH1 : muHu);
+            }
+            const int v = G ? 0 : 1;
+            const bool c1b = x < n && x + 2 * h >= n, c0b = x < n && x + 4 * h >= n;
+            const bool c3b = x + 2 * h < n && x + 6 * h >= n;
+            sc *o = out + (size_t)(4 * f) * h + i;
+            sc_store(o, s);
+            sc u;
+            const sc r1a = *reinterpret_cast<const sc *>(&Z.r1[v][0]), r1b = *reinterpret_cast<const sc *>(&Z.r1[v][1]);
+            const sc r0a = *reinterpret_cast<const sc *>(&Z.r0[v][0]), r0b = *reinterpret_cast<const sc *>(&Z.r0[v][1]);
+            const sc r1 = c1b ? r1b : r1a, r0x = c0b ? r0b : r0a, r0y = c3b ? r0b : r0a;
+            mm(u, s, r1); sc_store(o + h, u);
+            mm(t, u, r0y); sc_store(o + 3 * (size_t)h, t);
+            mm(u, s, r0x); sc_store(o + 2 * (size_t)h, u);
+        }
+    }
+    block_reduce_store<2>(acc, partial);
+}
+void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
+                           ScD *msm_scal, ScD *partial, hipStream_t st) {
+    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
+    hipLaunchKernelGGL(k_ipp_prep_deep2, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, z,
+                       AS_SC(msm_scal), AS_SC(partial));
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
+                       AS_SC(msm_scal + 16 * (size_t)args.h), 1u, 0);
+    BPG_HIP(hipGetLastError());
+}
 __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a, const sc *__restrict__ b,
                                                        const sc *__restrict__ yipm, IppRoundArgs A, uint32_t M,
                                                        const sc *__restrict__ wG, const sc *__restrict__ wH,
@@ -1824,6 +2141,19 @@ void launch_gather_niels(const NielsD *src, uint32_t count, uint32_t stride, uin
     if (!count) return;
     hipLaunchKernelGGL(k_gather_niels, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(src), count, stride, offset,
                        AS_GEN(dst));
+    BPG_HIP(hipGetLastError());
+}
+__global__ __launch_bounds__(64) void k_niels_neg(const gen *__restrict__ in, gen *__restrict__ out, uint32_t count) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count) return;
+    gen p;
+    gen_load(p, in + j);
+    gen_cneg(p, true);
+    gen_store(out + j, p);
+}
+void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_niels_neg, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(in), AS_GEN(out), count);
     BPG_HIP(hipGetLastError());
 }
 // Montgomery form -> canonical (MSM scalars from the IPP tail weights)

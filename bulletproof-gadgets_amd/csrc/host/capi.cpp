@@ -146,8 +146,13 @@ int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode) {
     return 0;
 }
 int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode) {
-    if (!ctx || mode < -1 || mode > 1) return -1;
+    if (!ctx || mode < -1 || mode > 2) return -1;
     ctx->strat.fold_pairs = mode;
+    return 0;
+}
+int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes) {
+    if (!ctx || lanes < -1) return -1;
+    ctx->strat.ipp_tail = lanes;
     return 0;
 }
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {

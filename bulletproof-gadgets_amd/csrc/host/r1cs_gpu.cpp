@@ -76,6 +76,15 @@ static bool env_off(const char *name) {
 }
 bool Strategy::tables() const { return fold_tables >= 0 ? fold_tables != 0 : !env_off("BPG_FOLD_TABLES"); }
 bool Strategy::pairs() const { return fold_pairs >= 0 ? fold_pairs != 0 : !env_off("BPG_FOLD_PAIRS"); }
+uint32_t Strategy::tail() const {
+    if (ipp_tail >= 0) return (uint32_t)ipp_tail;
+    static const uint32_t env = [] { const char *e = getenv("BPG_IPP_TAIL"); return e ? (uint32_t)atoi(e) : 4096u; }();
+    return env;
+}
+int Strategy::group() const {
+    if (fold_pairs >= 0) return fold_pairs == 0 ? 1 : fold_pairs == 1 ? 2 : 3;
+    return env_off("BPG_FOLD_PAIRS") ? 1 : env_off("BPG_FOLD_TRIPLES") ? 2 : 3;
+}
 
 static std::mutex g_cache_mu;
 static std::string g_cache_dir;
@@ -148,8 +157,8 @@ std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uin
         std::shared_ptr<GenSet> gs(new GenSet());
         gs->device = device;
         gs->N = cap;
-        BPG_HIP(hipMalloc(&gs->G, (size_t)cap * sizeof(dev::NielsD)));
-        BPG_HIP(hipMalloc(&gs->H, (size_t)cap * sizeof(dev::NielsD)));
+        BPG_HIP(hipMalloc(&gs->G, 2 * (size_t)cap * sizeof(dev::NielsD)));
+        BPG_HIP(hipMalloc(&gs->H, 2 * (size_t)cap * sizeof(dev::NielsD)));
         const std::string dir = gens_cache_dir();
         bool loaded = false;
         if (!dir.empty()) {
@@ -194,6 +203,9 @@ std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uin
                 }
             }
         }
+        launch_niels_neg(gs->G, gs->G + cap, cap, 0);
+        launch_niels_neg(gs->H, gs->H + cap, cap, 0);
+        BPG_HIP(hipDeviceSynchronize());
         full = gs;
         gens_from_cache = loaded;
         gens_ms += now_ms() - t0;
@@ -207,10 +219,12 @@ std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uin
     sl->N = N / world;
     sl->rank = rank;
     sl->world = world;
-    BPG_HIP(hipMalloc(&sl->G, (size_t)sl->N * sizeof(dev::NielsD)));
-    BPG_HIP(hipMalloc(&sl->H, (size_t)sl->N * sizeof(dev::NielsD)));
+    BPG_HIP(hipMalloc(&sl->G, 2 * (size_t)sl->N * sizeof(dev::NielsD)));
+    BPG_HIP(hipMalloc(&sl->H, 2 * (size_t)sl->N * sizeof(dev::NielsD)));
     launch_gather_niels(full->G, sl->N, world, rank, sl->G, 0);
     launch_gather_niels(full->H, sl->N, world, rank, sl->H, 0);
+    launch_niels_neg(sl->G, sl->G + sl->N, sl->N, 0);
+    launch_niels_neg(sl->H, sl->H + sl->N, sl->N, 0);
     BPG_HIP(hipDeviceSynchronize());
     slices[key] = sl;
     return sl;
@@ -275,7 +289,7 @@ struct Workspace : dev::ProfSink {
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
     DBuf wide, sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
-        ynwR, pts, okflag, wG, wH, wloc, wconv;
+        ynwR, pts, okflag, wG, wH, wloc, wconv, f3tab;
     PtD *rows_host = nullptr;        // pinned, 8 x 64 rows
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
@@ -283,6 +297,7 @@ struct Workspace : dev::ProfSink {
     dev::ArgStage fold_stage;        // IPP fold kernel arguments
     dev::ArgStage comb_stage;        // table-fold kernel arguments
     dev::ArgStage fold2_stage;       // two-round Straus fold kernel arguments
+    dev::ArgStage fold3_stage;       // three-round Straus fold kernel arguments
     hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
     void sync() {
         BPG_HIP(hipEventRecord(done_ev, st));
@@ -297,14 +312,16 @@ struct Workspace : dev::ProfSink {
         if (comb_stage.dev) (void)hipFree(comb_stage.dev);
         if (comb_stage.host) (void)hipHostFree(comb_stage.host);
         if (comb_stage.copied) (void)hipEventDestroy(comb_stage.copied);
-        if (fold2_stage.dev) (void)hipFree(fold2_stage.dev);
-        if (fold2_stage.host) (void)hipHostFree(fold2_stage.host);
-        if (fold2_stage.copied) (void)hipEventDestroy(fold2_stage.copied);
+        for (dev::ArgStage *a : {&fold2_stage, &fold3_stage}) {
+            if (a->dev) (void)hipFree(a->dev);
+            if (a->host) (void)hipHostFree(a->host);
+            if (a->copied) (void)hipEventDestroy(a->copied);
+        }
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&wide, &sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
-                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag, &wG, &wH, &wloc, &wconv};
+                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag, &wG, &wH, &wloc, &wconv, &f3tab};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -534,7 +551,7 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
     DeviceContext::get(device);
     Workspace &ws = thread_workspace(device);
     ws.small.grow((size_t)n * sizeof(ScD) + 64);
-    ws.pts.grow((size_t)n * sizeof(NielsD) + 64);
+    ws.pts.grow(2 * (size_t)n * sizeof(NielsD) + 64);   // points, then their negations
     ws.okflag.grow(64);
     std::vector<ScD> s(n ? n : 1);
     for (uint32_t i = 0; i < n; i++) s[i] = to_dev(Scalar::reduce(scalars + 32 * (size_t)i));
@@ -545,9 +562,10 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
     int one = 1;
     BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, ws.st));
     launch_decompress(as<uint32_t>(ws.gh), as<NielsD>(ws.pts), as<int>(ws.okflag), n, ws.st);
+    launch_niels_neg(as<NielsD>(ws.pts), as<NielsD>(ws.pts) + n, n, ws.st);
     int ok = 0;
     BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, ws.st));
-    MsmSeg seg{as<ScD>(ws.small), ws.pts.p, n, 0};
+    MsmSeg seg{as<ScD>(ws.small), ws.pts.p, n, 0, (int64_t)n};
     MsmPlan p = ws.msm->enqueue(&seg, 1, 1, ws.rows_host, MSM_NIELS);
     ws.sync();
     if (!ok) return -1;
@@ -745,10 +763,11 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
     MsmPlan pA{}, pS{};
     const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
+    const int64_t gneg = gs->N;             // their negations follow each vector
     if (nl) {
-        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0},
-                          {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0},
-                          {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1}};
+        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg},
+                          {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg},
+                          {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg}};
         int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
         pA = ws.msm->enqueue(segA, 3, 2, rowsA, MSM_NIELS);
         ws.prof_end(ph);
@@ -766,7 +785,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         }
         launch_wide_reduce(wd, nl, world, rank, as<ScD>(ws.sL), st);
         launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(ws.sR), st);
-        MsmSeg segS[2] = {{as<ScD>(ws.sL), G0, nl, 0}, {as<ScD>(ws.sR), H0, nl, 0}};
+        MsmSeg segS[2] = {{as<ScD>(ws.sL), G0, nl, 0, gneg}, {as<ScD>(ws.sR), H0, nl, 0, gneg}};
         int ph = ws.prof_begin("msm_commit", 2.0 * nl * (64 + 32));
         pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
         ws.prof_end(ph);
@@ -891,12 +910,14 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     Scalar wch = T.challenge_scalar("w");
     Point Qp; mul_B(Qp, wch);
     // Q in both base formats: cached for jobs over folded generators, affine
-    // Niels for jobs over the level-0 generators
-    ws.Q.grow(sizeof(PtD) + sizeof(NielsD));
+    // Niels (Q, then -Q) for jobs over the level-0 generators
+    ws.Q.grow(sizeof(PtD) + 2 * sizeof(NielsD));
     {
-        uint8_t qb[sizeof(PtD) + sizeof(NielsD)];
+        uint8_t qb[sizeof(PtD) + 2 * sizeof(NielsD)];
+        Point Qneg; pt_neg(Qneg, Qp);
         pt_to_dev_cached(reinterpret_cast<uint32_t *>(qb), Qp);
         pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD)), Qp);
+        pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD) + sizeof(NielsD)), Qneg);
         memcpy(ws.small_host + 3000, qb, sizeof(qb));
         BPG_HIP(hipMemcpyAsync(ws.Q.p, ws.small_host + 3000, sizeof(qb), hipMemcpyHostToDevice, st));
     }
@@ -925,27 +946,28 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     if (Nl >= 2) {
         for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(Nl / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(Nl / 2) * sizeof(PtD)); }
     }
-    // Round pairs: after round k the fold is left pending (Ghat stays at level
-    // k); round k+1's MSM expands each level-(k+1) base into its two level-k
-    // points, and level k+2 is built from level k in one pass (comb tables from
-    // the level-0 generators, else the three-scalar Straus fold).
-    const bool pairs = cs.strat.pairs();
-    Scalar rho_p[4];   // pending fold's scalars (G a/b, H a/b)
-    bool pend = false;
+    // Round groups: after round k the fold is left pending (Ghat stays at
+    // level k); round k+d's MSM expands each level-(k+d) base into its 2^d
+    // level-k points, and after the group's last round one pass builds the
+    // next level from level k: comb tables from the level-0 generators (a
+    // pair), else the three- (pair) or seven-scalar (triple) Straus fold.
+    const int group_cfg = sharded ? std::min(cs.strat.group(), 2) : cs.strat.group();
+    Scalar rho_h[2][4];   // the pending rounds' fold scalars (G a/b, H a/b), oldest first
+    int depth = 0;        // pending levels: Ghat at level k, this round at level k + depth
     int cur = -1;      // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
     // Tail (DESIGN.md "IPP tail without folds"): once a materialised level is
     // short, the remaining rounds keep it and weight its points instead of
     // folding them (each fold there is a latency-bound launch). The sharded
     // prover always ends in the tail: its last local round's fold is needed
     // (as weights) for the final generator of each rank.
-    static const uint32_t tail_len = [] { const char *e = getenv("BPG_IPP_TAIL"); return e ? (uint32_t)atoi(e) : 4096u; }();
+    const uint32_t tail_len = cs.strat.tail();
     bool tail = false;
     uint32_t M = 0;
     uint32_t len = Nl;
     uint32_t k = 0;
     for (; len != 1; k++) {
         const uint32_t h = len / 2;
-        if (!tail && !pend && cur >= 0 && len <= tail_len && len >= (sharded ? 2u : 4u)) {
+        if (!tail && depth == 0 && cur >= 0 && len <= tail_len && len >= (sharded ? 2u : 4u)) {
             tail = true;
             M = len;
             ws.wG.grow((size_t)M * sizeof(ScD) + 64);
@@ -963,10 +985,12 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         const void *Gm = cur < 0 ? G0 : Gh, *Hm = cur < 0 ? H0 : Hh;
         const void *Qb = mfmt == MSM_NIELS ? (const void *)Qn : (const void *)Qc;
         const size_t ps = mfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
+        // Niels jobs gather negated level-0 generators / -Q for negative digits
+        const int64_t gn = mfmt == MSM_NIELS ? gneg : 0, qn = mfmt == MSM_NIELS ? 1 : 0;
+        MsmSeg seg[MSM_MAX_SEGS];
         auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
-        MsmSeg seg[10];
         int nseg;
-        const bool lazy = pend;
+        const bool lazy = depth == 1;
         const size_t hh = h;
         if (tail) {
             launch_ipp_prep_tail(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, M, as<ScD>(ws.wG),
@@ -980,24 +1004,40 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
             const uint32_t h0 = 2 * h;
             LazyArgs Z;
             Z.h0 = h0;
-            Z.rGa = mont(rho_p[0]); Z.rGb = mont(rho_p[1]); Z.rHa = mont(rho_p[2]); Z.rHb = mont(rho_p[3]);
+            Z.rGa = mont(rho_h[0][0]); Z.rGb = mont(rho_h[0][1]); Z.rHa = mont(rho_h[0][2]); Z.rHb = mont(rho_h[0][3]);
             launch_ipp_prep_lazy(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
-            MsmSeg sl[10] = {{ms, at(Gm, h), h, 0}, {ms + hh, at(Gm, h + h0), h, 0}, {ms + 2 * hh, Hm, h, 0},
-                             {ms + 3 * hh, at(Hm, h0), h, 0}, {ms + 8 * hh, Qb, 1, 0},
-                             {ms + 4 * hh, Gm, h, 1}, {ms + 5 * hh, at(Gm, h0), h, 1},
-                             {ms + 6 * hh, at(Hm, h), h, 1}, {ms + 7 * hh, at(Hm, h + h0), h, 1},
-                             {ms + 8 * hh + 1, Qb, 1, 1}};
+            MsmSeg sl[10] = {{ms, at(Gm, h), h, 0, gn}, {ms + hh, at(Gm, h + h0), h, 0, gn}, {ms + 2 * hh, Hm, h, 0, gn},
+                             {ms + 3 * hh, at(Hm, h0), h, 0, gn}, {ms + 8 * hh, Qb, 1, 0, qn},
+                             {ms + 4 * hh, Gm, h, 1, gn}, {ms + 5 * hh, at(Gm, h0), h, 1, gn},
+                             {ms + 6 * hh, at(Hm, h), h, 1, gn}, {ms + 7 * hh, at(Hm, h + h0), h, 1, gn},
+                             {ms + 8 * hh + 1, Qb, 1, 1, qn}};
             std::copy(sl, sl + 10, seg);
             nseg = 10;
+        } else if (depth == 2) {
+            // bases at level k+2 expanded into level k: family f, term t at
+            // out[(4f + t) h], point offset x0(f) + 2h t
+            Deep2Args Z;
+            for (int v = 0; v < 2; v++)
+                for (int c = 0; c < 2; c++) { Z.r0[v][c] = mont(rho_h[0][2 * v + c]); Z.r1[v][c] = mont(rho_h[1][2 * v + c]); }
+            launch_ipp_prep_deep2(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
+            nseg = 0;
+            for (int f = 0; f < 4; f++) {
+                const void *B = (f & 1) ? Hm : Gm;
+                const size_t x0 = (f == 0 || f == 3) ? hh : 0;
+                for (int t = 0; t < 4; t++)
+                    seg[nseg++] = {ms + (size_t)(4 * f + t) * hh, at(B, x0 + 2 * hh * t), h, (uint32_t)(f >> 1), gn};
+                if (f == 1) seg[nseg++] = {ms + 16 * hh, Qb, 1, 0, qn};
+            }
+            seg[nseg++] = {ms + 16 * hh + 1, Qb, 1, 1, qn};
         } else {
             launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-            MsmSeg sl[6] = {{ms, at(Gm, h), h, 0}, {ms + hh, Hm, h, 0}, {ms + 4 * hh, Qb, 1, 0},
-                            {ms + 2 * hh, Gm, h, 1}, {ms + 3 * hh, at(Hm, h), h, 1},
-                            {ms + 4 * hh + 1, Qb, 1, 1}};
+            MsmSeg sl[6] = {{ms, at(Gm, h), h, 0, gn}, {ms + hh, Hm, h, 0, gn}, {ms + 4 * hh, Qb, 1, 0, qn},
+                            {ms + 2 * hh, Gm, h, 1, gn}, {ms + 3 * hh, at(Hm, h), h, 1, gn},
+                            {ms + 4 * hh + 1, Qb, 1, 1, qn}};
             std::copy(sl, sl + 6, seg);
             nseg = 6;
         }
-        int ph = ws.prof_begin("msm_ipp", ((tail ? 2.0 * M : lazy ? 8.0 * h : 4.0 * h) + 2) * (64 + 32));
+        int ph = ws.prof_begin("msm_ipp", ((tail ? 2.0 * M : (4.0 * h) * (1 << depth)) + 2) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, mfmt);
         ws.prof_end(ph);
         ws.sync();
@@ -1024,10 +1064,22 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
             if (h > 1 || sharded)
                 launch_ipp_tail_weights(as<ScD>(ws.wG), as<ScD>(ws.wH), M, h, nl, mont(rGa), mont(rGb), mont(rHa),
                                         mont(rHb), st);
-        } else if (lazy) {
-            pend = false;
-            if (h > 1) {
-                // level k+1 from level k-1: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
+        } else if (h > 1) {
+            const int group = (comb && cur < 0) ? 2 : group_cfg;
+            const Scalar rnow[4] = {rGa, rGb, rHa, rHb};
+            if (depth + 1 < group) {   // level k + depth + 1 stays implicit
+                std::copy(rnow, rnow + 4, rho_h[depth]);
+                depth++;
+            } else if (depth == 0) {
+                PtD *Gn = as<PtD>(ws.Gp[nxt]), *Hn = as<PtD>(ws.Hp[nxt]);
+                launch_ipp_fold_points(Gh, Hh, gfmt, h, nl, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
+                                       ws.fold_stage, st);
+                Gh = Gn; Hh = Hn;
+                cur = nxt;
+                gfmt = MSM_CACHED;
+            } else if (depth == 1) {
+                // level k+2 from level k: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
+                const Scalar *rho_p = rho_h[0];
                 const uint32_t h1 = h, h0 = 2 * h;
                 std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)nl - h1, (int64_t)nl, (int64_t)nl - h0,
                                             (int64_t)nl - h0 - h1};
@@ -1035,7 +1087,6 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 for (int64_t c : cut) if (c >= 0 && c < (int64_t)h1) starts.push_back((uint32_t)c);
                 std::sort(starts.begin(), starts.end());
                 starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
-                const Scalar r1[4] = {rGa, rGb, rHa, rHb};
                 ScD coef[2][COMB_MAXRANGE][3];
                 const bool table = comb && cur < 0;
                 CombArgs C{};
@@ -1046,7 +1097,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                     const bool b1 = i < nl && i + h1 >= nl, b0 = i < nl && i + h0 >= nl,
                                b0h = i + h1 < nl && i + h1 + h0 >= nl;
                     for (int v = 0; v < 2; v++) {
-                        const Scalar c1 = r1[2 * v + (b1 ? 1 : 0)];
+                        const Scalar c1 = rnow[2 * v + (b1 ? 1 : 0)];
                         const Scalar c2 = rho_p[2 * v + (b0 ? 1 : 0)];
                         const Scalar c3 = c1 * rho_p[2 * v + (b0h ? 1 : 0)];
                         if (table) {
@@ -1073,18 +1124,46 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 Gh = ws.Gp[nxt].p; Hh = ws.Hp[nxt].p;
                 cur = nxt;
                 gfmt = MSM_CACHED;
-            }
-        } else if (h > 1) {
-            if (pairs || (comb && cur < 0)) {
-                rho_p[0] = rGa; rho_p[1] = rGb; rho_p[2] = rHa; rho_p[3] = rHb;   // level k+1 stays implicit
-                pend = true;
+                depth = 0;
             } else {
-                PtD *Gn = as<PtD>(ws.Gp[nxt]), *Hn = as<PtD>(ws.Hp[nxt]);
-                launch_ipp_fold_points(Gh, Hh, gfmt, h, nl, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
-                                       ws.fold_stage, st);
-                Gh = Gn; Hh = Hn;
+                // level k+3 from level k: out_i = sum_{t<8} c_t P_{i + t hq}, point
+                // t = 4 b0 + 2 b1 + b2 reached through round k+2 (lane i), round
+                // k+1 (lane i + b2 hq) and round k (lane i + b2 hq + 2 b1 hq);
+                // each set bit contributes its round's scalar for that lane's class
+                const uint32_t hq = h;
+                const Scalar *rr[3] = {rho_h[0], rho_h[1], rnow};
+                std::vector<uint32_t> starts = {0};
+                for (int j = 0; j <= 8; j++) {
+                    const int64_t c = (int64_t)nl - (int64_t)j * hq;
+                    if (c > 0 && c < (int64_t)hq) starts.push_back((uint32_t)c);
+                }
+                std::sort(starts.begin(), starts.end());
+                starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+                if (starts.size() > COMB_MAXRANGE) throw std::runtime_error("fold3 ranges");
+                ScD coef[2][COMB_MAXRANGE][7];
+                auto cls = [&](uint64_t x, uint64_t half) { return x < nl && x + half >= nl ? 1 : 0; };
+                for (size_t r = 0; r < starts.size(); r++) {
+                    const uint64_t i = starts[r];
+                    for (int t = 1; t < 8; t++) {
+                        const int b0 = (t >> 2) & 1, b1 = (t >> 1) & 1, b2 = t & 1;
+                        const uint64_t x2 = i, x1 = i + (uint64_t)b2 * hq, x0 = x1 + (uint64_t)b1 * 2 * hq;
+                        for (int v = 0; v < 2; v++) {
+                            Scalar c = Scalar::one();
+                            if (b2) c = c * rr[2][2 * v + cls(x2, hq)];
+                            if (b1) c = c * rr[1][2 * v + cls(x1, 2 * (uint64_t)hq)];
+                            if (b0) c = c * rr[0][2 * v + cls(x0, 4 * (uint64_t)hq)];
+                            coef[v][r][t - 1] = to_dev(c);
+                        }
+                    }
+                }
+                const size_t tb = ipp_fold3_table_bytes(hq, (uint32_t)starts.size());
+                ws.f3tab.grow(tb);
+                launch_ipp_fold3(Gh, Hh, gfmt, hq, (uint32_t)starts.size(), starts.data(), coef, as<PtD>(ws.Gp[nxt]),
+                                 as<PtD>(ws.Hp[nxt]), ws.f3tab.p, ws.f3tab.cap, ws.fold3_stage, st);
+                Gh = ws.Gp[nxt].p; Hh = ws.Hp[nxt].p;
                 cur = nxt;
                 gfmt = MSM_CACHED;
+                depth = 0;
             }
         }
         lam = lam * uinv;
@@ -1322,7 +1401,7 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
         memcpy(comp.data() + (8 + m + k) * (size_t)32, ipp + 64 * k, 32);
         memcpy(comp.data() + (8 + m + lgn + k) * (size_t)32, ipp + 64 * k + 32, 32);
     }
-    ws.pts.grow((size_t)ns * sizeof(NielsD) + 64);
+    ws.pts.grow(2 * (size_t)ns * sizeof(NielsD) + 64);   // points, then their negations
     ws.okflag.grow(64);
     ws.mscal.grow((size_t)ns * 32 + (size_t)ns * sizeof(ScD) + 64);
     uint32_t *compd = as<uint32_t>(ws.mscal);
@@ -1331,6 +1410,7 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     int one = 1;
     BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
     launch_decompress(compd, as<NielsD>(ws.pts), as<int>(ws.okflag), ns, st);
+    launch_niels_neg(as<NielsD>(ws.pts), as<NielsD>(ws.pts) + ns, ns, st);
     int ok = 0;
     BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, st));
     ws.sync();
@@ -1346,8 +1426,9 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
     const uint64_t j0 = (uint64_t)N * shard / nshards, j1 = (uint64_t)N * (shard + 1) / nshards;
     const uint32_t cnt = (uint32_t)(j1 - j0);
-    MsmSeg seg[3] = {{as<ScD>(ws.gh) + j0, gs->G + j0, cnt, 0}, {as<ScD>(ws.gh) + N + j0, gs->H + j0, cnt, 0},
-                     {sscal, ws.pts.p, ns, 0}};
+    const int64_t gneg = gs->N;   // negated generators follow each vector
+    MsmSeg seg[3] = {{as<ScD>(ws.gh) + j0, gs->G + j0, cnt, 0, gneg}, {as<ScD>(ws.gh) + N + j0, gs->H + j0, cnt, 0, gneg},
+                     {sscal, ws.pts.p, ns, 0, (int64_t)ns}};
     MsmPlan pl = ws.msm->enqueue(seg, shard == 0 ? 3 : 2, 1, ws.rows_host, MSM_NIELS);
     ws.sync();
     Point R;

@@ -32,6 +32,8 @@ struct GenSet {
     int device = 0;
     uint32_t N = 0;                 // points per vector
     uint32_t rank = 0, world = 1;
+    // G, H: N points each, followed in the same allocation by their negations
+    // (G[N + i] = -G[i]): a negative MSM digit gathers -G_i (MsmSeg::negofs = N)
     dev::NielsD *G = nullptr, *H = nullptr;
     ~GenSet();
 };
@@ -49,8 +51,13 @@ struct CombTables {
 // 0 off, 1 on. Proof bytes are identical under every strategy.
 struct Strategy {
     int fold_tables = -1, fold_pairs = -1;
+    int ipp_tail = -1;   // IPP tail threshold in lanes (-1: env BPG_IPP_TAIL, else 4096)
+    uint32_t tail() const;
     bool tables() const;
     bool pairs() const;
+    // rounds folded together after the comb pass: 1 (one fold per round),
+    // 2 (pairs) or 3 (triples: fold_pairs 2, the default)
+    int group() const;
 };
 // Per-device state shared by all threads: the generator sets and comb
 // tables (circuit-independent, so derived once), the fixed-base tables of

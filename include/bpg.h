@@ -140,11 +140,20 @@ void bpg_ctx_destroy(bpg_ctx *ctx);
  *     per device) fold IPP rounds 0-1 in one table pass; 0: per-round
  *     variable-base fold; -1 (default): on unless env BPG_FOLD_TABLES=0
  *     (tables are skipped when they do not fit in free HBM).
- *   fold_pairs 1: rounds k, k+1 fold together (level k+2 from level k by a
- *     three-scalar Straus pass); 0: one fold per round; -1 (default): on
- *     unless env BPG_FOLD_PAIRS=0. */
+ *   fold_pairs 2: after the comb pass, rounds k, k+1, k+2 fold together
+ *     (level k+3 from level k by a seven-scalar Straus pass; rounds k+1, k+2
+ *     expand their bases into level-k points); 1: rounds fold in pairs
+ *     (three-scalar Straus pass); 0: one fold per round; -1 (default): 2,
+ *     or 1 with env BPG_FOLD_TRIPLES=0, or 0 with env BPG_FOLD_PAIRS=0. The
+ *     sharded prover folds at most in pairs. */
 int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode);
 int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
+/* IPP tail threshold of `ctx`'s calls: once a materialised generator level
+ * has at most `lanes` points, the remaining rounds weight its points instead
+ * of folding them (-1, the default: env BPG_IPP_TAIL, else 4096). Proof bytes
+ * are identical for every threshold; small values exercise the fold passes on
+ * small circuits. */
+int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes);
 
 /* Cold-setup breakdown of the device `ctx` is on: out[0] ms spent deriving
  * (or loading) generators, out[1] ms building comb tables, out[2] 1 if the

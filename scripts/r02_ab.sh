@@ -5,8 +5,14 @@
 set -o pipefail
 mkdir -p gpurun_out
 R=${R:-r02e}
+# PARITY_LIB: run the parity tests on that variant library instead of the default
+# SKIP_PARITY=1: the caller ran the tests already
+if [ "${SKIP_PARITY:-0}" != 1 ]; then
+if [ -n "$PARITY_LIB" ]; then export BPG_LIB_PATH=$PARITY_LIB; fi
 timeout -k 10 600 python -u -m pytest tests/test_gpu_fullsize.py "tests/test_gpu_parity.py::test_fold_strategy_bit_exact" \
   -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${R}_parity.log 2>&1 || exit $?
+unset BPG_LIB_PATH
+fi
 for rep in 1 2; do
   for v in default $AB; do
     name=${v%%=*}; lib=${v#*=}

@@ -110,15 +110,19 @@ def test_fixture_bit_exact(bpg, resources, name):
     assert S.verify_statement(name.encode(), fx["inst"], proof, coms, fx["gadgets"])
 
 
-@pytest.mark.parametrize("tables,pairs", [(0, 0), (1, 0), (0, 1), (1, 1), (-1, -1)])
+@pytest.mark.parametrize("tables,pairs,tail", [(0, 0, -1), (1, 0, -1), (0, 1, -1), (1, 1, -1), (-1, -1, -1),
+                                               (1, 2, 4), (0, 2, 4), (1, 1, 4), (0, 2, 16), (-1, -1, 8)])
 @pytest.mark.parametrize("name", ["bounds_check", "less_than", "example", "inequality", "or5"])
-def test_fold_strategy_bit_exact(bpg, resources, name, tables, pairs):
+def test_fold_strategy_bit_exact(bpg, resources, name, tables, pairs, tail):
     """Every IPP fold strategy of a context (per-round variable-base fold;
     comb-table pass for rounds 0-1 with a lazily expanded round-1 MSM; round
     pairs folded by the three-scalar Straus pass with lazily expanded
-    odd-round MSMs; the default) gives the oracle's bytes through the inner
-    ABI (bpg_r1cs_prove). The fixtures put n - N/2 on both sides of N/4, so
-    every lane class of the two-round passes occurs."""
+    odd-round MSMs; round triples folded by the seven-scalar Straus pass with
+    bases expanded two levels deep; the default) gives the oracle's bytes
+    through the inner ABI (bpg_r1cs_prove). A small IPP tail threshold makes
+    the fold passes run on these small circuits (the default tail would take
+    over right after the comb pass). The fixtures put n - N/2 on both sides
+    of N/4, so every lane class of the two-round passes occurs."""
     fx = read_fixture(os.path.join(resources, name))
     seed = 900 + len(name)
     st = S.synthesize_prover(fx["inst"], fx["wtns"], fx["gadgets"], seed)
@@ -126,7 +130,7 @@ def test_fold_strategy_bit_exact(bpg, resources, name, tables, pairs):
     ent = S.entropy_for(st)
     o_proof, o_V = O.r1cs_prove(name.encode(), flat, ent)
     c = bpg.Context(0)
-    c.set_strategy(tables, pairs)
+    c.set_strategy(tables, pairs, tail)
     proof, V = c.r1cs_prove(name.encode(), flat.view(), ent)
     assert V == o_V
     assert proof == o_proof

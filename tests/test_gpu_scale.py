@@ -68,15 +68,16 @@ def test_full_size_verify_and_strategies(bpg, W, cfg):
     syn = bpg.Synth(inst, wit, gad)
     ent = bytes([cfg]) * 32
     proofs = []
-    # (comb tables, round-pair folds): the production default, table pass +
-    # Straus pair folds, Straus pair folds only, one variable-base fold per
-    # round; each through its own context (strategies are per context)
-    for tables, pairs in ((-1, -1), (1, 1), (0, 1), (0, 0)):
+    # (comb tables, round grouping): the production default (table pass +
+    # Straus triple folds), table pass + Straus pair folds, Straus triple
+    # folds only, Straus pair folds only, one variable-base fold per round;
+    # each through its own context (strategies are per context)
+    for tables, pairs in ((-1, -1), (1, 1), (0, 2), (0, 1), (0, 0)):
         c = bpg.Context(0)
         c.set_strategy(tables, pairs)
         p, V = c.r1cs_prove(b"scale", syn.view, ent)
         proofs.append(p)
-    assert proofs[0] == proofs[1] == proofs[2] == proofs[3]
+    assert all(p == proofs[0] for p in proofs)
     proof = proofs[0]
     N = 1
     while N < syn.n:
