@@ -338,6 +338,7 @@ def main():
         "latency_ms_single_proof": round(single_ms, 1),
         "cold_setup_ms": round(prepare_ms, 1),
         "cold_setup_breakdown_ms": {"generators": round(setup["gens_ms"], 1), "comb_tables": round(setup["comb_ms"], 1),
+                                    "comb_tables_alloc": round(setup["comb_alloc_ms"], 1),
                                     "generators_from_disk_cache": setup["gens_from_cache"]},
         "phase_ms_single_proof": single_phases,
         "roofline": roof,

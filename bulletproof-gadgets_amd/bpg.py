@@ -340,9 +340,9 @@ class Context:
             raise BpgError("bad strategy")
 
     def setup_stats(self):
-        arr = (ctypes.c_double * 3)()
-        lib().bpg_ctx_setup_stats(self.h, arr, 3)
-        return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2])}
+        arr = (ctypes.c_double * 4)()
+        lib().bpg_ctx_setup_stats(self.h, arr, 4)
+        return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2]), "comb_alloc_ms": arr[3]}
 
     def msm(self, scalars, points):
         out = ctypes.create_string_buffer(32)

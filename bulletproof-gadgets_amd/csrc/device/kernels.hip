@@ -270,6 +270,9 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
 // holding its digit; rank = popcount of that mask below the lane.
 // ---------------------------------------------------------------------------
 // Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
+#ifndef RS_UNSTABLE_EARLY
+#define RS_UNSTABLE_EARLY 1   // passes before the last rank by LDS atomics (not stable)
+#endif
 #define RS_MAXBINS 256
 #define RS_MAXTILES (2048 + 4096)   // tiles of a job: <= 2048 full ones + one partial per row
 #define RS_BLOCK 256
@@ -317,7 +320,11 @@ __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist,
 // rank keys within their digit, the iteration is reordered by digit in LDS,
 // then written out so that lanes with consecutive LDS slots of one digit
 // write consecutive addresses.
-template <int RS_BITS>
+// STABLE = false (every pass but the last of an LSD sort: the next pass
+// reorders by a higher digit anyway, and equal keys are interchangeable in
+// the MSM): keys are ranked within their digit by LDS atomics instead of the
+// wave ballots.
+template <int RS_BITS, bool STABLE>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                          int shift, const uint32_t *__restrict__ tiles, uint32_t nb,
                                                          const uint32_t *__restrict__ hist,
@@ -325,7 +332,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
                                                          uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
     constexpr uint32_t RS_BINS = 1u << RS_BITS;
     __shared__ uint32_t base[RS_BINS], lstart[RS_BINS], tot[RS_BINS];
-    __shared__ uint32_t cnt[RS_ROUNDS][RS_BLOCK / 64][RS_BINS];
+    __shared__ uint32_t cnt[STABLE ? RS_ROUNDS : 1][RS_BLOCK / 64][RS_BINS];   // ballot ranking only
     __shared__ uint32_t lk[RS_ITER], lv[RS_ITER];
     const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull);
@@ -351,10 +358,44 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
     if (t < RS_BINS) base[t] = rstart + lstart[t] - cr + (hist[t * nb + blockIdx.x] - p0);
     const uint64_t t0 = TL[0], t1 = TL[1];
     for (uint64_t it = t0; it < t1; it += RS_ITER) {
+        uint32_t kk[RS_ROUNDS], vv[RS_ROUNDS], dd[RS_ROUNDS], rk[RS_ROUNDS];
+        if constexpr (!STABLE) {
+            if (t < RS_BINS) tot[t] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < RS_ROUNDS; r++) {
+                const uint64_t idx = it + (uint64_t)r * RS_BLOCK + t;
+                const bool ok = idx < t1;
+                kk[r] = ok ? kin[idx] : 0u;
+                vv[r] = ok ? vin[idx] : 0u;
+                const uint32_t d = (kk[r] >> shift) & (RS_BINS - 1);
+                dd[r] = ok ? d : 0xffffffffu;
+                rk[r] = ok ? atomicAdd(&tot[d], 1u) : 0u;
+            }
+            __syncthreads();
+            if (t < RS_BINS) lstart[t] = tot[t];
+            __syncthreads();
+            for (uint32_t d = 1; d < RS_BINS; d <<= 1) {   // inclusive scan of tot -> exclusive starts
+                uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
+                __syncthreads();
+                if (t < RS_BINS) lstart[t] += a;
+                __syncthreads();
+            }
+            if (t < RS_BINS) lstart[t] -= tot[t];
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < RS_ROUNDS; r++) {
+                if (dd[r] != 0xffffffffu) {
+                    const uint32_t pos = lstart[dd[r]] + rk[r];
+                    lk[pos] = kk[r];
+                    lv[pos] = vv[r];
+                }
+            }
+            __syncthreads();
+        } else {
         uint32_t *cz = &cnt[0][0][0];
         for (uint32_t j = t; j < RS_ROUNDS * (RS_BLOCK / 64) * RS_BINS; j += RS_BLOCK) cz[j] = 0;
         __syncthreads();
-        uint32_t kk[RS_ROUNDS], vv[RS_ROUNDS], dd[RS_ROUNDS], rk[RS_ROUNDS];
 #pragma unroll
         for (int r = 0; r < RS_ROUNDS; r++) {
             const uint64_t idx = it + (uint64_t)r * RS_BLOCK + t;
@@ -398,6 +439,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
             }
         }
         __syncthreads();
+        }
         const uint32_t n_it = (uint32_t)((t1 - it) < RS_ITER ? (t1 - it) : RS_ITER);
         for (uint32_t i = t; i < n_it; i += RS_BLOCK) {
             const uint32_t key = lk[i];
@@ -753,17 +795,25 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
     for (int shift = 0; shift < key_bits; shift += bits) {
+        // only the last pass must keep the order of equal digits
+        const bool last = !RS_UNSTABLE_EARLY || shift + bits >= key_bits;
         if (bits == 8)
             hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         else
             hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nt, total);
-        if (bits == 8)
-            hipLaunchKernelGGL(k_rs_scatter<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist, total,
-                               k2, v2);
+        if (bits == 8 && last)
+            hipLaunchKernelGGL((k_rs_scatter<8, true>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
+                               total, k2, v2);
+        else if (bits == 8)
+            hipLaunchKernelGGL((k_rs_scatter<8, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
+                               total, k2, v2);
+        else if (last)
+            hipLaunchKernelGGL((k_rs_scatter<7, true>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
+                               total, k2, v2);
         else
-            hipLaunchKernelGGL(k_rs_scatter<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist, total,
-                               k2, v2);
+            hipLaunchKernelGGL((k_rs_scatter<7, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
+                               total, k2, v2);
         std::swap(k, k2);
         std::swap(v, v2);
     }
@@ -1820,6 +1870,12 @@ void comb_digits(const uint8_t s[32], int8_t e[64]) {
     for (int i = 0; i < 64; i++) e[i] = (int8_t)(i < COMB_WIN ? v[i] : 0);
 }
 // ---------------------------------------------------------------------------
+// One generator per lane. Entries go out as affine Niels, so each needs
+// 1/Z: the entries of a chunk of COMB_BATCH consecutive multiples are first
+// parked in their own slots as packed (X, Y, Z) with the running product of
+// the Z's in registers, then one inversion and a backward walk give every
+// 1/Z (Montgomery's trick: 3M per entry instead of an inversion each).
+#define COMB_BATCH (COMB_ENT < 16 ? COMB_ENT : 16)
 __global__ __launch_bounds__(64) void k_comb_build(const gen *__restrict__ gens, uint32_t j0, uint32_t ntab,
                                                    uint4 *__restrict__ tab) {
     const uint32_t jj = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1834,11 +1890,44 @@ __global__ __launch_bounds__(64) void k_comb_build(const gen *__restrict__ gens,
         gec pc;
         ge_to_cached(pc, pw);
         ge q = pw;
-        for (int d = 0; d < COMB_ENT; d++) {
-            if (d) ge_add_c(q, q, pc);
-            gen e;
-            ge_to_niels(e, q);
-            genp_store(tab + ((size_t)(w * COMB_ENT + d) * ntab + jj) * 6, e);
+        for (int d0 = 0; d0 < COMB_ENT; d0 += COMB_BATCH) {
+            fe pre[COMB_BATCH];
+#pragma unroll
+            for (int b = 0; b < COMB_BATCH; b++) {
+                const int d = d0 + b;
+                if (d) ge_add_c(q, q, pc);
+                uint32_t xw[24];
+                fe_tow(xw, q.X); fe_tow(xw + 8, q.Y); fe_tow(xw + 16, q.Z);
+                uint4 *slot = tab + ((size_t)(w * COMB_ENT + d) * ntab + jj) * 6;
+#pragma unroll
+                for (int k = 0; k < 6; k++) slot[k] = make_uint4(xw[4 * k], xw[4 * k + 1], xw[4 * k + 2], xw[4 * k + 3]);
+                if (b) fe_mul(pre[b], pre[b - 1], q.Z); else pre[b] = q.Z;
+            }
+            fe inv;
+            fe_invert(inv, pre[COMB_BATCH - 1]);
+#pragma unroll
+            for (int b = COMB_BATCH - 1; b >= 0; b--) {
+                uint4 *slot = tab + ((size_t)(w * COMB_ENT + d0 + b) * ntab + jj) * 6;
+                uint4 s6[6];
+#pragma unroll
+                for (int k = 0; k < 6; k++) s6[k] = slot[k];
+                fe X = fe_from_words(s6[0].x, s6[0].y, s6[0].z, s6[0].w, s6[1].x, s6[1].y, s6[1].z, s6[1].w);
+                fe Y = fe_from_words(s6[2].x, s6[2].y, s6[2].z, s6[2].w, s6[3].x, s6[3].y, s6[3].z, s6[3].w);
+                fe zi, x, y, t;
+                if (b) {
+                    fe Z = fe_from_words(s6[4].x, s6[4].y, s6[4].z, s6[4].w, s6[5].x, s6[5].y, s6[5].z, s6[5].w);
+                    fe_mul(zi, inv, pre[b - 1]);
+                    fe_mul(inv, inv, Z);
+                } else {
+                    zi = inv;
+                }
+                fe_mul(x, X, zi); fe_mul(y, Y, zi);
+                gen e;
+                fe_add(e.YpX, y, x); fe_sub(e.YmX, y, x);
+                fe_mul(t, x, y); fe_mul(e.T2d, t, FE_D2);
+                e.pad[0] = e.pad[1] = 0;
+                genp_store(slot, e);
+            }
         }
         ge_dbl(pw, q);   // R^(w+1) P = 2 (COMB_ENT R^w P)
     }

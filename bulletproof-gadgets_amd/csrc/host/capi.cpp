@@ -159,8 +159,8 @@ int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
     if (!ctx) return -1;
     DeviceContext &c = DeviceContext::get(ctx->device);
     std::lock_guard<std::mutex> lk(c.mu);
-    const double v[3] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0};
-    for (int i = 0; i < n && i < 3; i++) out[i] = v[i];
+    const double v[4] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms};
+    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
     return 0;
 }
 

@@ -260,6 +260,7 @@ std::shared_ptr<CombTables> DeviceContext::comb(const std::shared_ptr<const GenS
         (void)hipGetLastError();
         return nullptr;
     }
+    comb_alloc_ms += now_ms() - t0;
     launch_comb_build(gs->G, h1, ntab, t->tabG, 0);
     launch_comb_build(gs->H, h1, ntab, t->tabH, 0);
     BPG_HIP(hipDeviceSynchronize());

@@ -71,6 +71,7 @@ struct DeviceContext {
     PtD *tabB = nullptr, *tabBb = nullptr;
     PtD *Bb = nullptr;                  // B_blinding as a device point
     double gens_ms = 0, comb_ms = 0;    // time spent deriving / building (cold-setup breakdown)
+    double comb_alloc_ms = 0;           // of comb_ms: allocating the table memory
     bool gens_from_cache = false;
     static DeviceContext &get(int device);
     // Thread-safe. world == 1: a full set with at least N points (grown on

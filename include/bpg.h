@@ -157,7 +157,8 @@ int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes);
 
 /* Cold-setup breakdown of the device `ctx` is on: out[0] ms spent deriving
  * (or loading) generators, out[1] ms building comb tables, out[2] 1 if the
- * generators came from the on-disk cache. */
+ * generators came from the on-disk cache, out[3] ms of out[1] spent
+ * allocating the tables' memory. */
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n);
 
 /* Ensure G_i, H_i for i < capacity are resident (BulletproofGens::new(cap,1),

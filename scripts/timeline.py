@@ -5,7 +5,9 @@ Prints the traced span, the union of kernel intervals (time the GPU had at
 least one kernel resident), the mean number of concurrently resident kernels,
 and per kernel: calls, summed duration, and its share of the busy union
 (each instant of the union is split evenly over the kernels resident then).
-usage: timeline.py <run_results.db> [t_from_frac] [out.md]
+Also: time with k kernels resident (k = 0, 1, 2, 3, 4+) and the time at
+least one VALU-heavy kernel (MSM pass 1, comb/Straus folds) was resident.
+usage: timeline.py <run_results.db> [t_from_frac] [out.md] [t_to_frac]
 """
 import re
 import sqlite3
@@ -27,9 +29,15 @@ def main():
     ev = [(int(s), int(e), short(n)) for n, s, e in c.execute("select name, %s, %s from kernels" % (s_col, e_col))]
     ev.sort()
     t_lo, t_hi = ev[0][0], max(e for _, e, _ in ev)
+    frac1 = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0
     cut = t_lo + frac0 * (t_hi - t_lo)
-    ev = [x for x in ev if x[0] >= cut]
+    cut1 = t_lo + frac1 * (t_hi - t_lo)
+    ev = [x for x in ev if x[0] >= cut and x[1] <= cut1]
     t_lo = ev[0][0]
+    t_hi = max(e for _, e, _ in ev)
+    heavy = ("k_rbk_pass<true", "k_ipp_comb_fold", "k_ipp_fold2", "k_ipp_fold3")
+    hist = [0] * 5
+    heavy_t = 0
     pts = []
     for i, (s, e, n) in enumerate(ev):
         pts.append((s, 1, i))
@@ -46,6 +54,10 @@ def main():
         calls[n] = calls.get(n, 0) + 1
         dur[n] = dur.get(n, 0) + (e - s)
     for t, d, i in pts:
+        if t > last:
+            hist[min(len(active), 4)] += t - last
+            if any(ev[j][2].startswith(heavy) for j in active):
+                heavy_t += t - last
         if active and t > last:
             dt = t - last
             busy += dt
@@ -60,7 +72,9 @@ def main():
             active.discard(i)
     span = t_hi - t_lo
     lines = ["span %.2f ms, busy union %.2f ms (%.1f%%), mean resident kernels while busy %.2f, kernels %d" %
-             (span / 1e6, busy / 1e6, 100 * busy / span, conc / max(busy, 1), len(ev)), "",
+             (span / 1e6, busy / 1e6, 100 * busy / span, conc / max(busy, 1), len(ev)),
+             "time with 0/1/2/3/4+ kernels resident: " + " / ".join("%.1f%%" % (100 * h / span) for h in hist) +
+             "; a VALU-heavy kernel resident %.1f%%" % (100 * heavy_t / span), "",
              "| kernel | calls | sum dur ms | avg us | share of busy ms | share % |", "|---|---|---|---|---|---|"]
     for n in sorted(share, key=lambda k: -share[k]):
         lines.append("| %s | %d | %.2f | %.1f | %.2f | %.1f%% |" % (n, calls[n], dur[n] / 1e6, dur[n] / calls[n] / 1e3,
