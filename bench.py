@@ -51,10 +51,12 @@ def parse():
                     help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
                          "one HIP stream each (default 24 with >= 16 cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("prove", "verify", "latency"), default="prove",
+    ap.add_argument("--mode", choices=("prove", "verify", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification); latency: one proof at a time, sharded over all "
-                         "ranks (bpg_prove_prepared). Secondary lines, not the headline metric")
+                         "ranks (bpg_prove_prepared); statements: distinct statements end to end through c_prove "
+                         "(parse + synthesis + upload + prove, prove.rs:37-82). Secondary lines, not the headline "
+                         "metric")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="processes of the all-core CPU leg (default: the host cores this rank may use, at most 16)")
@@ -197,6 +199,9 @@ def main():
     # 16 proofs per host thread per step; the timed steps run as one
     # continuous pipeline (below), so the end-of-batch drain is paid once
     batch = a.batch or 16 * threads
+
+    if a.mode == "statements":
+        return bench_statements(a, bpg, dist, D, rank, world, W)
 
     # every rank proves its own statement, except in latency mode, where the
     # ranks share ONE proof of one statement
@@ -458,6 +463,62 @@ def bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W):
                    "parallelism": "one proof sharded over %d ranks (lanes i = j*%d + rank)" % (world, world)},
         "latency_ms": round(dt / a.steps * 1e3, 1), "phase_ms_last_proof_rank0": phases,
         "prepare_ms": round(prepare_ms, 1),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_statements(a, bpg, dist, D, rank, world, W):
+    """The reference's prove() (prove.rs:37-82) for DISTINCT statements, end to
+    end: every proof parses its own statement text, synthesises the circuit on
+    the host, uploads it (flattened view, transposed constraints) and proves
+    it, through the reference C-ABI (c_prove), on `threads` host threads at
+    once (one HIP stream each; ctypes releases the GIL). The statement texts
+    (config-5 family, seeded) are generated before timing. A step = `batch`
+    statements; value = statements x q / wall time."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    threads = a.threads or 16
+    batch = a.batch or 2 * threads
+    texts = [W.config5(50000 + 100003 * rank + i) for i in range(batch * (a.steps + a.warmup))]
+    q = bpg.Synth(*texts[0]).q
+
+    def one(t):
+        return bpg.prove("bench", t[0], t[1], t[2])
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    pool = ThreadPoolExecutor(threads)
+    list(pool.map(one, texts[:batch * a.warmup]))
+    barrier()
+    t0 = time.perf_counter()
+    outs = list(pool.map(one, texts[batch * a.warmup:]))
+    barrier()
+    dt = time.perf_counter() - t0
+    # the worker threads (and their per-thread device workspaces) end here,
+    # while the HIP runtime is certainly still up
+    pool.shutdown(wait=True)
+    if dist is not None:
+        dt = D.max_over_ranks(dt)
+    last = texts[-1]
+    if rank == 0 and not bpg.verify("bench", last[0], outs[-1][0], outs[-1][1], last[2]):
+        raise SystemExit("bench: a statement's proof failed to verify")
+    n_st = batch * a.steps * world
+    out = {
+        "metric": "R1CS prove constraints/sec end to end over distinct statements (c_prove: parse + synthesis + "
+                  "upload + prove) at %d MI355X" % world,
+        "value": round(n_st * q / dt, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32 (255-bit integer field/scalar arithmetic)",
+        "data": "synthetic: %d distinct seeded config-5 statements per rank" % (batch * a.steps),
+        "config": {"workload": W.NAMES[5], "q_constraints": q, "statements_per_step_per_gpu": batch,
+                   "host_threads_per_gpu": threads},
+        "statements_per_s": round(n_st / dt, 2),
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -62,7 +62,9 @@ void launch_compress(const NielsD *in, uint32_t *out, uint32_t count, hipStream_
 void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count, hipStream_t st);
 
 // -------------------------------------------------------------- MSM
+#ifndef MSM_MAX_SEGS
 #define MSM_MAX_SEGS 18   // segments per MSM job (a round-triple IPP job: 2 x (8 + 1))
+#endif
 #define MSM_CACHED 0   // bases are cached points (PtD)
 #define MSM_NIELS 1    // bases are affine Niels points (NielsD)
 struct MsmSeg {

@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "dev_field.h"
 #include "kernels.h"
@@ -270,6 +271,15 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
 // holding its digit; rank = popcount of that mask below the lane.
 // ---------------------------------------------------------------------------
 // Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
+// RS_SEGSORT 1: two-digit sorts run the high digit tiled, then each (row, high
+// digit) segment by its low digit in one block (k_rs_segsort: no global
+// histogram, no stable ranking). Measured 67.8 vs 71.9 M constraints/s
+// (profiles/r02v_ab_segsort.txt): its entries land at scattered 4-byte
+// positions inside the segment, where the tiled scatter writes runs staged in
+// LDS. Off by default.
+#ifndef RS_SEGSORT
+#define RS_SEGSORT 0
+#endif
 #ifndef RS_UNSTABLE_EARLY
 #define RS_UNSTABLE_EARLY 1   // passes before the last rank by LDS atomics (not stable)
 #endif
@@ -454,6 +464,67 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
     }
 }
 
+// Two-digit sorts run MSD-first: the high digit by the (unstable) tiled pass
+// above, then every (row, high digit) segment on its own by the low digit
+// (k_rs_segsort): one block per segment counts its low digits in LDS and
+// places each entry by an LDS atomic — no global histogram, no stable
+// ranking (equal keys are interchangeable in the MSM).
+// Segment table: per row (first tile rowfirst[r]) and high digit d,
+// seg[2 (r bins + d)] = start, [+1] = length, from the pass's tile histograms.
+__global__ __launch_bounds__(256) void k_rs_segs(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ total,
+                                                 const uint32_t *__restrict__ tiles,
+                                                 const uint32_t *__restrict__ rowfirst, uint32_t nt, uint32_t bins,
+                                                 uint32_t *__restrict__ seg) {
+    __shared__ uint32_t sc_[256];
+    const uint32_t row = blockIdx.x, t = threadIdx.x;
+    const uint32_t *TL = tiles + 5 * rowfirst[row];
+    const uint32_t r0 = TL[2], r1 = TL[3], rstart = TL[4];
+    uint32_t cnt = 0;
+    if (t < bins) cnt = (r1 < nt ? hist[t * nt + r1] : total[t]) - hist[t * nt + r0];
+    sc_[t] = cnt;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint32_t a = t >= d ? sc_[t - d] : 0u;
+        __syncthreads();
+        sc_[t] += a;
+        __syncthreads();
+    }
+    if (t < bins) {
+        seg[2 * ((size_t)row * bins + t)] = rstart + sc_[t] - cnt;
+        seg[2 * ((size_t)row * bins + t) + 1] = cnt;
+    }
+}
+template <int LBITS>
+__global__ __launch_bounds__(256) void k_rs_segsort(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                    const uint32_t *__restrict__ seg, uint32_t *__restrict__ kout,
+                                                    uint32_t *__restrict__ vout) {
+    constexpr uint32_t LB = 1u << LBITS;
+    __shared__ uint32_t cnt[LB], off[LB];
+    const uint32_t t = threadIdx.x;
+    const uint32_t s0 = seg[2 * (size_t)blockIdx.x], n = seg[2 * (size_t)blockIdx.x + 1];
+    if (n == 0) return;
+    if (t < LB) cnt[t] = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += 256) atomicAdd(&cnt[kin[s0 + i] & (LB - 1)], 1u);
+    __syncthreads();
+    if (t < LB) off[t] = cnt[t];
+    __syncthreads();
+    for (uint32_t d = 1; d < LB; d <<= 1) {   // inclusive scan -> exclusive starts
+        const uint32_t a = (t < LB && t >= d) ? off[t - d] : 0u;
+        __syncthreads();
+        if (t < LB) off[t] += a;
+        __syncthreads();
+    }
+    if (t < LB) off[t] -= cnt[t];
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += 256) {
+        const uint32_t key = kin[s0 + i], val = vin[s0 + i];
+        const uint32_t pos = atomicAdd(&off[key & (LB - 1)], 1u);
+        kout[s0 + pos] = key;
+        vout[s0 + pos] = val;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Run reduction over the sorted entries, by fixed chunks of RBK_T entries per
 // thread (keys/values staged through LDS with one pad word per RBK_T, so
@@ -517,6 +588,16 @@ template <bool NEGC> DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) {
 // issued before entry i's addition (two base registers used in turn, so no
 // copy between them); otherwise entries are slots (key or key|RBK_FILL,
 // extended point at the same index) of the previous pass.
+// Latency-bound point kernels (run merges, the final run sums): compiled for
+// BPG_LAT_WAVES waves per SIMD. Capping them at 4 (128 VGPRs, so they hold
+// fewer registers while waiting on loads next to other streams' VALU-bound
+// kernels) measured no gain (70.6 vs 70.9 M, profiles/r02s_ab_latwaves.txt).
+#ifndef RBK_MERGE_PREFETCH
+#define RBK_MERGE_PREFETCH 0   // 1: merge passes load the next real slot's point ahead (no gain measured, profiles/r02u_ab_merge_prefetch.txt)
+#endif
+#ifndef BPG_LAT_WAVES
+#define BPG_LAT_WAVES 1
+#endif
 // RBK_PINGPONG: entry i+1's base is gathered into the other of two base
 // registers (no copy, more VGPRs); else into the one just consumed.
 #ifndef RBK_PINGPONG
@@ -526,7 +607,7 @@ template <bool NEGC> DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) {
 #define RBK_WAVES (RBK_PINGPONG ? 2 : 3)   // waves per SIMD the run reduction is compiled for
 #endif
 template <bool FIRST, int FMT, bool NEGC>
-__global__ __launch_bounds__(RBK_BLOCK, (FIRST && FMT == MSM_CACHED) ? 2 : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
+__global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACHED ? 2 : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         const ge *__restrict__ pin, SegTab T, uint64_t E,
                                                         uint32_t invalid, int cw, uint32_t *__restrict__ kout,
@@ -609,7 +690,7 @@ __global__ __launch_bounds__(RBK_BLOCK, (FIRST && FMT == MSM_CACHED) ? 2 : RBK_W
         }
         (void)pb;
 #endif
-    } else {
+    } else if (!RBK_MERGE_PREFETCH) {
         for (uint32_t i = 0; i < RBK_T; i++) {
             const uint32_t x = sk[rbk_lds(t * RBK_T + i)];
             const uint32_t k = RBK_KEY(x);
@@ -617,6 +698,33 @@ __global__ __launch_bounds__(RBK_BLOCK, (FIRST && FMT == MSM_CACHED) ? 2 : RBK_W
             if (k != cur) close_run(k);
             if (!(x & RBK_FILL)) {
                 ge p; ge_load(p, pin + gs + i);
+                ge_add(acc, acc, p);
+                real = true;
+            }
+        }
+    } else {
+        // slots of the previous pass: the point of the next real slot (not a
+        // filler) is in flight while the current one is added
+        const uint32_t *skt = sk + rbk_lds(t * RBK_T);
+        auto next_real = [&](uint32_t j) -> uint32_t {
+            for (; j < RBK_T; j++) {
+                const uint32_t x = skt[j];
+                if (RBK_KEY(x) == invalid) return RBK_T;
+                if (!(x & RBK_FILL)) return j;
+            }
+            return RBK_T;
+        };
+        uint32_t nr = next_real(0);
+        ge pn;
+        if (nr < RBK_T) ge_load(pn, pin + gs + nr);
+        for (uint32_t i = 0; i < RBK_T; i++) {
+            const uint32_t k = RBK_KEY(skt[i]);
+            if (k == invalid) break;
+            if (k != cur) close_run(k);
+            if (i == nr) {
+                const ge p = pn;
+                nr = next_real(i + 1);
+                if (nr < RBK_T) ge_load(pn, pin + gs + nr);
                 ge_add(acc, acc, p);
                 real = true;
             }
@@ -637,7 +745,7 @@ __global__ __launch_bounds__(RBK_BLOCK, (FIRST && FMT == MSM_CACHED) ? 2 : RBK_W
 }
 // After the last pass: the head slot of each run sums the run's real pieces
 // and owns the bucket (serial; long only for giant runs of structured digits).
-__global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
+__global__ __launch_bounds__(64, BPG_LAT_WAVES) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
                                                   uint64_t E, uint32_t invalid, int cw, ge *__restrict__ buckets,
                                                   uint8_t *__restrict__ bflag) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -662,7 +770,7 @@ __global__ __launch_bounds__(64) void k_rbk_final(const uint32_t *__restrict__ k
 DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict__ F, size_t i) {
     if (F[i]) ge_load(p, B + i); else ge_identity(p);
 }
-__global__ __launch_bounds__(64) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
+__global__ __launch_bounds__(64, 3) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
                                                    uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
                                                    ge *__restrict__ segA, ge *__restrict__ segT) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -775,7 +883,8 @@ void DBuf::grow(size_t need) {
 void MsmEngine::reserve(const MsmPlan &p) {
     size_t kb = p.E0 * 4;
     keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
-    sort_tmp_.grow((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256);   // radix-sort tile histograms + totals
+    // radix-sort tile histograms + totals, then the segment table (2 words per row and digit)
+    sort_tmp_.grow((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256 + (size_t)2 * RS_MAXBINS * p.rows * 4);
     rk_a_.grow(p.capE * 4); rp_a_.grow(p.capE * sizeof(ge));
     rk_b_.grow(p.capE * 4 / 4 + 1024); rp_b_.grow((p.capE / 4 + 256) * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
@@ -788,15 +897,38 @@ void MsmEngine::reserve(const MsmPlan &p) {
 // a row; tiles_dev: nt x {start, end, first tile of the row, one past its last
 // tile, row start}); swaps the buffer pointers to the sorted pair.
 static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2, int key_bits, const uint32_t *tiles,
-                       uint32_t nt, uint32_t *hist, hipStream_t st) {
+                       uint32_t nt, const uint32_t *rowfirst, uint32_t rows, uint32_t *hist, uint32_t *seg,
+                       hipStream_t st) {
     if (!nt || key_bits < 1) return;
     // 8-bit digits only where they save a pass (their scatter costs more LDS)
     const int bits = (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
+    const int passes = (key_bits + bits - 1) / bits;
+    if (passes == 2 && RS_SEGSORT) {
+        // high digit (bits [bits, key_bits), plus constant row bits) by the
+        // tiled pass, then each (row, high digit) segment by the low digit
+        const int shift = bits;
+        if (bits == 8) hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
+        else hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
+        hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nt, total);
+        if (bits == 8)
+            hipLaunchKernelGGL((k_rs_scatter<8, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
+                               total, k2, v2);
+        else
+            hipLaunchKernelGGL((k_rs_scatter<7, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
+                               total, k2, v2);
+        hipLaunchKernelGGL(k_rs_segs, dim3(rows), dim3(256), 0, st, hist, total, tiles, rowfirst, nt, bins, seg);
+        if (bits == 8)
+            hipLaunchKernelGGL(k_rs_segsort<8>, dim3(rows * bins), dim3(256), 0, st, k2, v2, seg, k, v);
+        else
+            hipLaunchKernelGGL(k_rs_segsort<7>, dim3(rows * bins), dim3(256), 0, st, k2, v2, seg, k, v);
+        BPG_HIP(hipGetLastError());
+        return;   // sorted pairs are back in (k, v)
+    }
     for (int shift = 0; shift < key_bits; shift += bits) {
-        // only the last pass must keep the order of equal digits
-        const bool last = !RS_UNSTABLE_EARLY || shift + bits >= key_bits;
+        // only the last of several passes must keep the order of equal digits
+        const bool last = passes > 1 && (!RS_UNSTABLE_EARLY || shift + bits >= key_bits);
         if (bits == 8)
             hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         else
@@ -886,12 +1018,14 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     tile = std::max<uint64_t>(RS_ITER, (tile + RS_ITER - 1) / RS_ITER * RS_ITER);
     if (!tiles_ev_) {
         BPG_HIP(hipEventCreateWithFlags(&tiles_ev_, hipEventDisableTiming));
-        BPG_HIP(hipHostMalloc((void **)&tiles_host_, (size_t)5 * RS_MAXTILES * 4, hipHostMallocDefault));
-        tiles_.grow((size_t)5 * RS_MAXTILES * 4);
+        // tile table (5 words per tile), then each row's first tile
+        BPG_HIP(hipHostMalloc((void **)&tiles_host_, (size_t)6 * RS_MAXTILES * 4, hipHostMallocDefault));
+        tiles_.grow((size_t)6 * RS_MAXTILES * 4);
     } else {
         event_wait(tiles_ev_);   // the previous job's upload has left the staging buffer
     }
     uint32_t nt = 0;
+    std::vector<uint32_t> rowfirst(p.rows);
     for (int r = 0; r < p.rows; r++) {
         const uint32_t m = (uint32_t)r % nmsm, w = (uint32_t)r / nmsm;
         const uint64_t rs = (uint64_t)w * total + moff[m];
@@ -904,8 +1038,11 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
             e[4] = (uint32_t)rs;
         }
         for (uint32_t k = t0; k < nt; k++) { tiles_host_[5 * k + 2] = t0; tiles_host_[5 * k + 3] = nt; }
+        rowfirst[r] = t0;
     }
-    BPG_HIP(hipMemcpyAsync(tiles_.p, tiles_host_, (size_t)5 * nt * 4, hipMemcpyHostToDevice, st_));
+    if (nt + p.rows > RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
+    memcpy(tiles_host_ + 5 * nt, rowfirst.data(), (size_t)p.rows * 4);
+    BPG_HIP(hipMemcpyAsync(tiles_.p, tiles_host_, (size_t)(5 * nt + p.rows) * 4, hipMemcpyHostToDevice, st_));
     BPG_HIP(hipEventRecord(tiles_ev_, st_));
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     uint8_t *bflag = (uint8_t *)bflag_.p;
@@ -914,7 +1051,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
                        (uint32_t)nmsm, (uint32_t)p.half, keys, vals);
     BPG_HIP(hipGetLastError());
-    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p, st_);
+    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt,
+               (const uint32_t *)tiles_.p + 5 * nt, (uint32_t)p.rows, (uint32_t *)sort_tmp_.p,
+               (uint32_t *)sort_tmp_.p + (size_t)RS_MAXBINS * (RS_MAXTILES + 1) + 64, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
     uint64_t E = p.E0;
     const uint32_t *kin = keys;

@@ -965,6 +965,9 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     bool tail = false;
     uint32_t M = 0;
     uint32_t len = Nl;
+    // a (= l(x), zero past the real lanes) is nonzero only on lanes < anz:
+    // anz = nl, then min(anz, h) after each round's fold
+    uint32_t anz = nl;
     uint32_t k = 0;
     for (; len != 1; k++) {
         const uint32_t h = len / 2;
@@ -1032,11 +1035,14 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
             seg[nseg++] = {ms + 16 * hh + 1, Qb, 1, 1, qn};
         } else {
             launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-            MsmSeg sl[6] = {{ms, at(Gm, h), h, 0, gn}, {ms + hh, Hm, h, 0, gn}, {ms + 4 * hh, Qb, 1, 0, qn},
-                            {ms + 2 * hh, Gm, h, 1, gn}, {ms + 3 * hh, at(Hm, h), h, 1, gn},
+            // points whose a-scalar is zero (padding lanes) are left out of
+            // the job: L's G part runs over a_lo, R's over a_hi
+            const uint32_t nLG = std::min(h, anz), nRG = anz > h ? std::min(h, anz - h) : 0u;
+            MsmSeg sl[6] = {{ms, at(Gm, h), nLG, 0, gn}, {ms + hh, Hm, h, 0, gn}, {ms + 4 * hh, Qb, 1, 0, qn},
+                            {ms + 2 * hh, Gm, nRG, 1, gn}, {ms + 3 * hh, at(Hm, h), h, 1, gn},
                             {ms + 4 * hh + 1, Qb, 1, 1, qn}};
-            std::copy(sl, sl + 6, seg);
-            nseg = 6;
+            nseg = 0;
+            for (const MsmSeg &x : sl) if (x.count) seg[nseg++] = x;
         }
         int ph = ws.prof_begin("msm_ipp", ((tail ? 2.0 * M : (4.0 * h) * (1 << depth)) + 2) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, mfmt);
@@ -1170,6 +1176,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         lam = lam * uinv;
         mu = mu * uk;
         len = h;
+        anz = std::min(anz, h);
     }
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1010, ws.a.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
     BPG_HIP(hipMemcpyAsync(ws.small_host + 1011, ws.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
