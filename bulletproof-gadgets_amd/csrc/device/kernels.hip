@@ -1813,6 +1813,7 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
 #ifndef BPG_FOLD3_WNAF
 #define BPG_FOLD3_WNAF 4
 #endif
+static_assert(BPG_FOLD3_WNAF >= 3 && BPG_FOLD3_WNAF <= 5, "fold3 NAF width (odd multiples up to 15P)");
 #define FOLDN_MAXSEG (2 * COMB_MAXRANGE)
 #define FOLDN_MAXOPS 640
 #define FOLDN_K 7
@@ -1825,7 +1826,7 @@ struct FoldNArgs {
     uint32_t hq, nseg;
     uint32_t start[FOLDN_MAXSEG], end[FOLDN_MAXSEG], blk0[FOLDN_MAXSEG + 1], vec[FOLDN_MAXSEG];
     uint32_t nops[FOLDN_MAXSEG], tail[FOLDN_MAXSEG];
-    // op: gap (8 bits) | point t - 1 << 8 (3 bits) | (m >> 1) << 11 (2 bits) | neg << 15
+    // op: gap (8 bits) | point t - 1 << 8 (3 bits) | (m >> 1) << 11 (3 bits) | neg << 15
     uint16_t ops[FOLDN_MAXSEG][FOLDN_MAXOPS];
 };
 DEVI void foldn_put(uint32_t *tb, const gec &c) {
@@ -1879,7 +1880,7 @@ __global__ __launch_bounds__(64, 1) void k_ipp_fold3(const FoldNArgs *__restrict
             }
         }
     }
-    auto entry = [&](uint32_t op) { return tb + (((op >> 8) & 7) * FOLDN_MULT + ((op >> 11) & 3)) * 40 * 64; };
+    auto entry = [&](uint32_t op) { return tb + (((op >> 8) & 7) * FOLDN_MULT + ((op >> 11) & 7)) * 40 * 64; };
     ge acc;
     {
         const uint32_t op = fold2_op(ops, 0);
