@@ -270,7 +270,6 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
 // Stable ranking inside a wave: 7 ballots give each lane the mask of lanes
 // holding its digit; rank = popcount of that mask below the lane.
 // ---------------------------------------------------------------------------
-// Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
 // RS_SEGSORT 1: two-digit sorts run the high digit tiled, then each (row, high
 // digit) segment by its low digit in one block (k_rs_segsort: no global
 // histogram, no stable ranking). Measured 67.8 vs 71.9 M constraints/s
@@ -280,6 +279,7 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
 #ifndef RS_SEGSORT
 #define RS_SEGSORT 0
 #endif
+// Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
 #ifndef RS_UNSTABLE_EARLY
 #define RS_UNSTABLE_EARLY 1   // passes before the last rank by LDS atomics (not stable)
 #endif
@@ -464,6 +464,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
     }
 }
 
+#if RS_SEGSORT
 // Two-digit sorts run MSD-first: the high digit by the (unstable) tiled pass
 // above, then every (row, high digit) segment on its own by the low digit
 // (k_rs_segsort): one block per segment counts its low digits in LDS and
@@ -494,18 +495,37 @@ __global__ __launch_bounds__(256) void k_rs_segs(const uint32_t *__restrict__ hi
         seg[2 * ((size_t)row * bins + t) + 1] = cnt;
     }
 }
+// One block per segment. Segments of up to RS_SEG_LDS entries are held in
+// registers, ranked by LDS atomics, placed in LDS and written out in order
+// (coalesced); longer ones (structured scalars) are placed straight into
+// global memory.
+#define RS_SEG_LDS 8192
 template <int LBITS>
 __global__ __launch_bounds__(256) void k_rs_segsort(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                     const uint32_t *__restrict__ seg, uint32_t *__restrict__ kout,
                                                     uint32_t *__restrict__ vout) {
     constexpr uint32_t LB = 1u << LBITS;
+    constexpr int PER = RS_SEG_LDS / 256;
     __shared__ uint32_t cnt[LB], off[LB];
+    __shared__ uint32_t lk[RS_SEG_LDS], lv[RS_SEG_LDS];
     const uint32_t t = threadIdx.x;
     const uint32_t s0 = seg[2 * (size_t)blockIdx.x], n = seg[2 * (size_t)blockIdx.x + 1];
     if (n == 0) return;
     if (t < LB) cnt[t] = 0;
     __syncthreads();
-    for (uint32_t i = t; i < n; i += 256) atomicAdd(&cnt[kin[s0 + i] & (LB - 1)], 1u);
+    const bool small = n <= RS_SEG_LDS;
+    uint32_t kr[PER], vr[PER];
+    if (small) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const uint32_t i = j * 256 + t;
+            kr[j] = i < n ? kin[s0 + i] : 0u;
+            vr[j] = i < n ? vin[s0 + i] : 0u;
+            if (i < n) atomicAdd(&cnt[kr[j] & (LB - 1)], 1u);
+        }
+    } else {
+        for (uint32_t i = t; i < n; i += 256) atomicAdd(&cnt[kin[s0 + i] & (LB - 1)], 1u);
+    }
     __syncthreads();
     if (t < LB) off[t] = cnt[t];
     __syncthreads();
@@ -517,6 +537,23 @@ __global__ __launch_bounds__(256) void k_rs_segsort(const uint32_t *__restrict__
     }
     if (t < LB) off[t] -= cnt[t];
     __syncthreads();
+    if (small) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const uint32_t i = j * 256 + t;
+            if (i < n) {
+                const uint32_t pos = atomicAdd(&off[kr[j] & (LB - 1)], 1u);
+                lk[pos] = kr[j];
+                lv[pos] = vr[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < n; i += 256) {
+            kout[s0 + i] = lk[i];
+            vout[s0 + i] = lv[i];
+        }
+        return;
+    }
     for (uint32_t i = t; i < n; i += 256) {
         const uint32_t key = kin[s0 + i], val = vin[s0 + i];
         const uint32_t pos = atomicAdd(&off[key & (LB - 1)], 1u);
@@ -524,6 +561,7 @@ __global__ __launch_bounds__(256) void k_rs_segsort(const uint32_t *__restrict__
         vout[s0 + pos] = val;
     }
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Run reduction over the sorted entries, by fixed chunks of RBK_T entries per
@@ -905,7 +943,8 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
     const int passes = (key_bits + bits - 1) / bits;
-    if (passes == 2 && RS_SEGSORT) {
+#if RS_SEGSORT
+    if (passes == 2 && key_bits >= 15) {   // the big jobs (c >= 15); small ones keep the tiled LSD passes
         // high digit (bits [bits, key_bits), plus constant row bits) by the
         // tiled pass, then each (row, high digit) segment by the low digit
         const int shift = bits;
@@ -926,6 +965,9 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
         BPG_HIP(hipGetLastError());
         return;   // sorted pairs are back in (k, v)
     }
+#else
+    (void)rowfirst; (void)rows; (void)seg;
+#endif
     for (int shift = 0; shift < key_bits; shift += bits) {
         // only the last of several passes must keep the order of equal digits
         const bool last = passes > 1 && (!RS_UNSTABLE_EARLY || shift + bits >= key_bits);

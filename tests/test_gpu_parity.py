@@ -62,6 +62,23 @@ def test_msm_structured_scalars(ctx):
     assert ctx.msm(ones, same) == O.msm(ones, same)
 
 
+def test_msm_large_structured(ctx):
+    """A job big enough for 16-bit windows (2^18 + 5 points: the two-digit
+    radix sort and the run merges at their full depth) with a quarter of the
+    scalars equal to 1 (one bucket of 65K entries: runs far longer than any
+    sort tile or reduction chunk), a quarter small, the rest random."""
+    rnd = random.Random(18)
+    n = (1 << 18) + 5
+    pts = rand_points(rnd, 97)
+    pts = [pts[i % 97] for i in range(n)]
+    vals = []
+    for i in range(n):
+        k = i % 4
+        v = [1, rnd.randrange(1 << 20), rnd.randrange(L), L - 1 - i][k]
+        vals.append(v.to_bytes(32, "little"))
+    assert ctx.msm(vals, pts) == O.msm(vals, pts)
+
+
 def test_msm_identity_and_invalid(ctx, bpg):
     assert ctx.msm([b"\0" * 32], [O.pedersen_gens()[0]]) == b"\0" * 32
     with pytest.raises(bpg.BpgError):
