@@ -51,10 +51,11 @@ def parse():
                     help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
                          "one HIP stream each (default 24 with >= 16 cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("prove", "verify", "latency", "statements"), default="prove",
+    ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification); latency: one proof at a time, sharded over all "
-                         "ranks (bpg_prove_prepared); statements: distinct statements end to end through c_prove "
+                         "ranks (bpg_prove_prepared); verify-sharded: one verification at a time, its mega-MSM "
+                         "split over all ranks; statements: distinct statements end to end through c_prove "
                          "(parse + synthesis + upload + prove, prove.rs:37-82). Secondary lines, not the headline "
                          "metric")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
@@ -205,7 +206,7 @@ def main():
 
     # every rank proves its own statement, except in latency mode, where the
     # ranks share ONE proof of one statement
-    srank = 0 if a.mode == "latency" else rank
+    srank = 0 if a.mode in ("latency", "verify-sharded") else rank
     inst, wit, gad = W.CONFIGS[a.config]() if a.config != 5 else W.config5(1005 + 7919 * srank)
     bpg.set_seed(1000 + srank)
     syn = bpg.Synth(inst, wit, gad)
@@ -229,6 +230,8 @@ def main():
 
     if a.mode == "verify":
         return bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropies, q, n, N, W)
+    if a.mode == "verify-sharded":
+        return bench_verify_sharded(a, bpg, ctx, syn, prep, D, dist, rank, world, q, n, N, W)
     if a.warmup:
         prep.prove_batch(b"bench", sum((entropies(1000 + s) for s in range(a.warmup)), []), threads)
     L = bpg.lib()
@@ -413,6 +416,61 @@ def bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropie
                    "parallelism": "independent verifications per GPU (%d ranks)" % world},
         "proofs_per_s": round(total / dt, 2),
         "latency_ms_single_verify": round(single_ms, 2),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_verify_sharded(a, bpg, ctx, syn, prep, D, dist, rank, world, q, n, N, W):
+    """Verifier::verify (verify.rs:71) one proof at a time with its mega-MSM
+    split over all ranks (bpg_r1cs_verify_shard on every rank, one all-gather
+    of 32-byte partial sums, dist.sharded_verify) — SURVEY §8e's second
+    option for "batch verify across GPUs", next to --mode verify's
+    independent proofs per rank. value = verifications x q / max-over-ranks
+    seconds; scaling strong (the work per verification is fixed)."""
+    import torch
+    proof = prep.prove_batch(b"bench", [b"\x07" * 32], 1)[0]
+    if dist is not None:   # every rank verifies rank 0's bytes
+        proof = D.all_gather_bytes(proof)[0]
+    V = _commitments(ctx, syn)
+
+    def verify(p):   # one rank: the unsharded verifier (no process group)
+        if dist is None:
+            return ctx.r1cs_verify(b"bench", syn.view, V, p)
+        return D.sharded_verify(bpg, ctx, b"bench", syn.view, V, p)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        if not verify(proof):
+            raise SystemExit("bench: a valid proof was rejected")
+    bad = bytearray(proof)
+    bad[-40] ^= 1
+    if verify(bytes(bad)):
+        raise SystemExit("bench: a tampered proof was accepted")
+    barrier()
+    t0 = time.perf_counter()
+    ok = all(verify(proof) for _ in range(a.steps))
+    barrier()
+    dt = time.perf_counter() - t0
+    if not ok:
+        raise SystemExit("bench: a valid proof was rejected in the timed region")
+    if dist is not None:
+        dt = D.max_over_ranks(dt)
+    out = {
+        "metric": "R1CS verify constraints/sec, one verification at a time sharded over %d MI355X" % world,
+        "value": round(a.steps * q / dt, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32 (255-bit integer field/scalar arithmetic)",
+        "data": "synthetic: seeded config-%d statement" % a.config,
+        "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
+                   "parallelism": "one verification's mega-MSM split over %d ranks" % world},
+        "latency_ms_verify": round(dt / a.steps * 1e3, 3),
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
