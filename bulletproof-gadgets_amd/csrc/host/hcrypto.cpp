@@ -15,27 +15,19 @@ static inline void st64(uint8_t *p, uint64_t x) { memcpy(p, &x, 8); }
 
 // ============================================================== scalars
 static const uint64_t LL[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0, 0x1000000000000000ULL};
+// Montgomery constants of l (R = 2^256): np = -l^-1 mod 2^64, r1 = R mod l,
+// r2 = R^2 mod l (the statement layer multiplies millions of scalars, so
+// these are plain constants rather than computed on first use behind a
+// thread-safe static guard)
 struct ScConsts {
     uint64_t np;
     uint64_t r2[4];
     uint64_t r1[4];
-    ScConsts() {
-        uint64_t inv = 1;
-        for (int i = 0; i < 7; i++) inv *= 2 - LL[0] * inv;
-        np = (uint64_t)0 - inv;
-        uint64_t x[4] = {1, 0, 0, 0};
-        for (int i = 0; i < 512; i++) {
-            u128 c = 0;
-            for (int k = 0; k < 4; k++) { c += (u128)x[k] + x[k]; x[k] = (uint64_t)c; c >>= 64; }
-            bool ge = true;
-            for (int k = 3; k >= 0; k--) { if (x[k] != LL[k]) { ge = x[k] > LL[k]; break; } }
-            if (ge) { u128 b = 0; for (int k = 0; k < 4; k++) { u128 d = (u128)x[k] - LL[k] - b; x[k] = (uint64_t)d; b = (d >> 64) & 1; } }
-            if (i == 255) memcpy(r1, x, 32);
-        }
-        memcpy(r2, x, 32);
-    }
 };
-static const ScConsts &scc() { static ScConsts c; return c; }
+static const ScConsts SCC = {0xd2b51da312547e1bULL,
+                             {0xa40611e3449c0f01ULL, 0xd00e1ba768859347ULL, 0xceec73d217f5be65ULL, 0x0399411b7c309a3dULL},
+                             {0xd6ec31748d98951dULL, 0xc6ef5bf4737dcf70ULL, 0xfffffffffffffffeULL, 0x0fffffffffffffffULL}};
+static inline const ScConsts &scc() { return SCC; }
 
 static inline bool geq_l(const uint64_t t[4]) {
     for (int i = 3; i >= 0; i--) { if (t[i] != LL[i]) return t[i] > LL[i]; }
@@ -45,7 +37,7 @@ static inline void sub_l(uint64_t t[4]) {
     u128 b = 0;
     for (int i = 0; i < 4; i++) { u128 d = (u128)t[i] - LL[i] - b; t[i] = (uint64_t)d; b = (d >> 64) & 1; }
 }
-static void reduce256(uint64_t t[4]) {
+static void reduce256_slow(uint64_t t[4]) {
     while (geq_l(t)) {
         uint64_t q = t[3] >> 60;
         if (q <= 1) { sub_l(t); continue; }
@@ -56,8 +48,13 @@ static void reduce256(uint64_t t[4]) {
         for (int i = 0; i < 4; i++) { u128 d = (u128)t[i] - ql[i] - b; t[i] = (uint64_t)d; b = (d >> 64) & 1; }
     }
 }
+// t < l whenever its top limb is below l's (l >= 2^252): the common case
+static inline void reduce256(uint64_t t[4]) {
+    if (t[3] < LL[3]) return;
+    reduce256_slow(t);
+}
 // CIOS Montgomery; a < 2^256, b < l -> result < l
-static void montmul(uint64_t r[4], const uint64_t a[4], const uint64_t b[4]) {
+static inline void montmul(uint64_t r[4], const uint64_t a[4], const uint64_t b[4]) {
     const uint64_t np = scc().np;
     uint64_t t[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 4; i++) {
@@ -117,7 +114,11 @@ Scalar operator-(const Scalar &a0, const Scalar &b0) {
     return r;
 }
 Scalar operator-(const Scalar &a) { return Scalar::zero() - a; }
+static inline bool is_one(const Scalar &x) { return x.v[0] == 1 && !x.v[1] && !x.v[2] && !x.v[3]; }
 Scalar operator*(const Scalar &a, const Scalar &b0) {
+    // unit coefficients are common in the statement layer's linear combinations
+    if (is_one(b0)) return a.reduced();
+    if (is_one(a)) return b0.reduced();
     Scalar b = b0.reduced(), t, r;
     montmul(t.v, a.v, b.v);
     montmul(r.v, t.v, scc().r2);

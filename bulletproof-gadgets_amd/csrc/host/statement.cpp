@@ -67,6 +67,20 @@ void ConstraintSystem::emit(const LC &lc) {
     }
     row_ptr_.push_back((uint32_t)term_var_.size());
 }
+void ConstraintSystem::emit_minus(const LC &lc, Var v) {
+    static const Scalar minus_one = -Scalar::one();
+    for (auto &x : lc.t) {
+        term_var_.push_back(x.first);
+        uint8_t b[32];
+        x.second.to_bytes(b);
+        term_coeff_.insert(term_coeff_.end(), b, b + 32);
+    }
+    term_var_.push_back(v);
+    uint8_t b[32];
+    minus_one.to_bytes(b);
+    term_coeff_.insert(term_coeff_.end(), b, b + 32);
+    row_ptr_.push_back((uint32_t)term_var_.size());
+}
 // r1cs Prover::multiply / Verifier::multiply: allocate (l, r, o), constrain
 // left - l = 0 and right - r = 0.
 ConstraintSystem::Triple ConstraintSystem::multiply(const LC &left, const LC &right) {
@@ -76,9 +90,12 @@ ConstraintSystem::Triple ConstraintSystem::multiply(const LC &left, const LC &ri
         Scalar l = eval(left), r = eval(right);
         aL_.push_back(l); aR_.push_back(r); aO_.push_back(l * r);
     }
-    Op op{true, left, right, t.l, t.r};
-    if (stack_.empty()) replay_mul(op);
-    else stack_.back().push_back(std::move(op));
+    if (stack_.empty()) {   // left - l = 0 and right - r = 0, without copying the combinations
+        emit_minus(left, t.l);
+        emit_minus(right, t.r);
+    } else {
+        stack_.back().push_back(Op{true, left, right, t.l, t.r});
+    }
     return t;
 }
 ConstraintSystem::Triple ConstraintSystem::allocate_multiplier(const Scalar *l, const Scalar *r) {
@@ -95,11 +112,8 @@ void ConstraintSystem::constrain(const LC &lc) {
 }
 void ConstraintSystem::replay_mul(const Op &op) {
     if (!stack_.empty()) { stack_.back().push_back(op); return; }
-    LC a = op.a, b = op.b;
-    a.t.push_back({op.lv, -Scalar::one()});
-    b.t.push_back({op.rv, -Scalar::one()});
-    emit(a);
-    emit(b);
+    emit_minus(op.a, op.lv);
+    emit_minus(op.b, op.rv);
 }
 void ConstraintSystem::push_buffer() { stack_.emplace_back(); cache_.emplace_back(); }
 void ConstraintSystem::rewind() {

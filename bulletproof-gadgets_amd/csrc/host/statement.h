@@ -74,6 +74,7 @@ class ConstraintSystem {
   private:
     Scalar eval(const LC &lc) const;
     void emit(const LC &lc);
+    void emit_minus(const LC &lc, Var v);   // emit lc - v (a multiplier's input constraint)
     bool prover_;
     uint32_t nvars_ = 0;
     std::vector<Scalar> aL_, aR_, aO_, v_, vb_;
