@@ -72,6 +72,7 @@ DEVI constexpr fe fe_from_words(const uint32_t w0, const uint32_t w1, const uint
 #define FE_C(name, a0, a1, a2, a3, a4, a5, a6, a7) \
     static __device__ __constant__ const fe name = fe_from_words(a0, a1, a2, a3, a4, a5, a6, a7);
 FE_C(FE_D, 0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du, 0x7779e898u, 0x8cc74079u, 0x2b6ffe73u, 0x52036ceeu)
+FE_C(FE_D_INV, 0xcdc9f843u, 0x25e0f276u, 0x4279542eu, 0x0b5dd698u, 0xcdb9cf66u, 0x2b162114u, 0x14d5ce43u, 0x40907ed2u)   // 1/d
 FE_C(FE_D2, 0x26b2f159u, 0xebd69b94u, 0x8283b156u, 0x00e0149au, 0xeef3d130u, 0x198e80f2u, 0x56dffce7u, 0x2406d9dcu)
 FE_C(FE_SQRT_M1, 0x4a0ea0b0u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u, 0x3dfbd7a7u, 0x2b4d0099u, 0x4fc1df0bu, 0x2b832480u)
 FE_C(FE_SQRT_AD_MINUS_ONE, 0x497b2e1bu, 0x7e97f6a0u, 0x1b7854bdu, 0xaf9d8e0cu, 0x31f5d1fdu, 0x0f3cfcc9u, 0x2b8348acu, 0x376931bfu)
@@ -476,6 +477,20 @@ DEVI void ge_madd(ge &r, const ge &p, const gen &q) {
 }
 DEVI void gen_cneg(gen &c, bool neg) {
     if (neg) { fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; fe_neg(c.T2d, c.T2d); }
+}
+// identity + q without the addition (a run's first entry): from Y+X, Y-X
+// and 2dT, (Y+X)-(Y-X) = 2X, (Y+X)+(Y-X) = 2Y and (2dT)/d = 2T give
+// (2X : 2Y : 2Z : 2T), with Z = 1 for an affine Niels point: 1M instead of
+// the 7M madd / 8M cached addition into the identity.
+DEVI void ge_from_niels(ge &r, const gen &q) {
+    fe_sub(r.X, q.YpX, q.YmX); fe_add(r.Y, q.YpX, q.YmX);
+    fe_zero(r.Z); r.Z.v[0] = 2;
+    fe_mul(r.T, q.T2d, FE_D_INV);
+}
+DEVI void ge_from_cached_t(ge &r, const gec &q) {   // uses 2dT (ge_from_cached below does not)
+    fe_sub(r.X, q.YpX, q.YmX); fe_add(r.Y, q.YpX, q.YmX);
+    r.Z = q.Z2;
+    fe_mul(r.T, q.T2d, FE_D_INV);
 }
 DEVI void gen_identity(gen &c) { fe_one(c.YpX); fe_one(c.YmX); fe_zero(c.T2d); c.pad[0] = c.pad[1] = 0; }
 // affine Niels as a cached point (2Z = 2)

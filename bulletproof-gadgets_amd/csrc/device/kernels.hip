@@ -621,6 +621,15 @@ template <bool NEGC> DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) {
     if (!NEGC) gec_cneg(p, neg);
     ge_add_c(acc, acc, p);
 }
+// the same into an accumulator that holds the identity: a conversion (1M)
+template <bool NEGC> DEVI void msm_init_loaded(ge &acc, gen &p, bool neg) {
+    if (!NEGC) gen_cneg(p, neg);
+    ge_from_niels(acc, p);
+}
+template <bool NEGC> DEVI void msm_init_loaded(ge &acc, gec &p, bool neg) {
+    if (!NEGC) gec_cneg(p, neg);
+    ge_from_cached_t(acc, p);
+}
 
 // FIRST: entries are (key, signed base index) and the gather of entry i+1 is
 // issued before entry i's addition (two base registers used in turn, so no
@@ -640,6 +649,11 @@ template <bool NEGC> DEVI void msm_add_loaded(ge &acc, gec &p, bool neg) {
 // registers (no copy, more VGPRs); else into the one just consumed.
 #ifndef RBK_PINGPONG
 #define RBK_PINGPONG 0
+#endif
+// RBK_FRESH0: a run's first point is converted or copied instead of being
+// added to the identity (pass-1 entry 0, merge passes, final run sums, comb fold)
+#ifndef RBK_FRESH0
+#define RBK_FRESH0 1
 #endif
 #ifndef RBK_WAVES
 #define RBK_WAVES (RBK_PINGPONG ? 2 : 3)   // waves per SIMD the run reduction is compiled for
@@ -722,7 +736,22 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
             if (!step(i + 1, pb, pa)) break;
         }
 #else
-        for (uint32_t i = 0; i < RBK_T; i++) {
+        uint32_t i0 = 0;
+#if RBK_FRESH0
+        // entry 0 starts every lane's chunk from the identity (its own run or
+        // the open head), the same step for the whole wave: its base is
+        // converted, not added (1M instead of 7M / 8M)
+        {
+            BT use = pa;
+            if (RBK_T > 1) {
+                const uint32_t kn = RBK_KEY(skt[1]);
+                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[1]);
+            }
+            if (!rbk_trash(first, cw)) { msm_init_loaded<NEGC>(acc, use, svt[0] >> 31); real = true; }
+            i0 = 1;
+        }
+#endif
+        for (uint32_t i = i0; i < RBK_T; i++) {
             BT use = pa;
             if (!step(i, use, pa)) break;
         }
@@ -736,7 +765,8 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
             if (k != cur) close_run(k);
             if (!(x & RBK_FILL)) {
                 ge p; ge_load(p, pin + gs + i);
-                ge_add(acc, acc, p);
+                if (real || !RBK_FRESH0) ge_add(acc, acc, p);
+                else acc = p;              // the run's first piece: acc is the identity
                 real = true;
             }
         }
@@ -763,7 +793,8 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
                 const ge p = pn;
                 nr = next_real(i + 1);
                 if (nr < RBK_T) ge_load(pn, pin + gs + nr);
-                ge_add(acc, acc, p);
+                if (real || !RBK_FRESH0) ge_add(acc, acc, p);
+                else acc = p;
                 real = true;
             }
         }
@@ -796,7 +827,8 @@ __global__ __launch_bounds__(64, BPG_LAT_WAVES) void k_rbk_final(const uint32_t 
     for (uint64_t j = i; j < E && RBK_KEY(keys[j]) == k; j++) {
         if (keys[j] & RBK_FILL) continue;
         ge_load(p, pts + j);
-        ge_add(acc, acc, p);
+        if (real || !RBK_FRESH0) ge_add(acc, acc, p);
+        else acc = p;
         real = true;
     }
     if (real) { ge_store(buckets + rbk_bucket(k, cw), acc); bflag[rbk_bucket(k, cw)] = 1; }
@@ -2136,11 +2168,14 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
     for (int k = 1; k < COMB_MAXRANGE; k++) if (k < (int)A.nrange && i >= A.rstart[k]) r = k;
     const uint4 *tab = reinterpret_cast<const uint4 *>(A.tab[v]);
     ge acc;
-    ge_identity(acc);
     {
         gen p;
         gen_load(p, reinterpret_cast<const gen *>(A.gens[v]) + i);
-        ge_madd(acc, acc, p);
+#if RBK_FRESH0
+        ge_from_niels(acc, p);   // identity + P_i (1M)
+#else
+        ge_identity(acc); ge_madd(acc, acc, p);
+#endif
     }
     for (int t = 0; t < 3; t++) {
         const uint32_t jj = i + (uint32_t)t * A.h1;

@@ -23,7 +23,8 @@ void sim_sc_add(const uint32_t *a, const uint32_t *b, uint32_t *r) { sc x, y, z;
 void sim_sc_sub(const uint32_t *a, const uint32_t *b, uint32_t *r) { sc x, y, z; memcpy(x.v, a, 32); memcpy(y.v, b, 32); sc_sub(z, x, y); memcpy(r, z.v, 32); }
 void sim_sc_reduce(const uint32_t *a, uint32_t *r) { sc x, z; memcpy(x.v, a, 32); sc_reduce(z, x); memcpy(r, z.v, 32); }
 // points: compressed in/out. op: 0 add, 1 sub, 2 add_cached, 3 sub_cached,
-// 4 dbl, 5 dbl without T then add (exercises the T-less doubling)
+// 4 dbl, 5 dbl without T then add (exercises the T-less doubling),
+// 9-12 identity-free run starts (Niels / cached -> extended, then + p)
 int sim_pt_op(int op, const uint32_t *a, const uint32_t *b, uint32_t *r) {
     ge p, q, s;
     if (!ristretto_decode(p, a) || !ristretto_decode(q, b)) return -1;
@@ -41,6 +42,14 @@ int sim_pt_op(int op, const uint32_t *a, const uint32_t *b, uint32_t *r) {
             gen qu; genp_unpack(qu, pk);
             gen_cneg(qu, op == 7);
             ge_madd(s, p, qu); break;
+        }
+        case 9: case 10: {  // run start of MSM pass 1 / comb fold: Niels -> extended (1M), then + p
+            gen qn; ge_to_niels(qn, q); gen_cneg(qn, op == 10);
+            ge t; ge_from_niels(t, qn); ge_add(s, t, p); break;
+        }
+        case 11: case 12: { // the same from a cached point (uses its 2dT)
+            gec c2 = qc; gec_cneg(c2, op == 12);
+            ge t; ge_from_cached_t(t, c2); ge_add(s, t, p); break;
         }
         default: {          // Niels -> cached (2Z = 2) path of the fold kernel
             gen qn; ge_to_niels(qn, q); gec c2; gen_to_cached(c2, qn); ge_add_c(s, p, c2); break;

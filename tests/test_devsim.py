@@ -141,7 +141,7 @@ def test_point_formulas_vs_oracle(sim):
         dbl = O.point_mul(two, a)
         four_plus = O.point_add(O.point_mul((4).to_bytes(32, "little"), a), b)
         for op, want in [(0, add), (1, sub), (2, add), (3, sub), (4, dbl), (5, four_plus), (6, add), (7, sub),
-                         (8, add)]:
+                         (8, add), (9, add), (10, sub), (11, add), (12, sub)]:
             assert sim.sim_pt_op(op, wa, wb, r) == 0
             assert bytes(r) == want, (op, i)
 
