@@ -1139,8 +1139,10 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         const uint32_t nblocks = (uint32_t)std::max<uint64_t>(1, (E + RBK_CHUNK - 1) / RBK_CHUNK);
         // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
         ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"),
-                     96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels
-                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);
+                     96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels;
+                     // each lane's first entry is a 1M conversion (RBK_FRESH0)
+                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0 -
+                         (RBK_FRESH0 ? (fmt == MSM_CACHED ? 7.0 : 6.0) * (double)((p.E0 + RBK_T - 1) / RBK_T) : 0.0));
         if (p.passes == 0 && fmt == MSM_NIELS && negc)
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, true>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
                                pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
