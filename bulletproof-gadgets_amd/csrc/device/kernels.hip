@@ -655,11 +655,14 @@ template <bool NEGC> DEVI void msm_init_loaded(ge &acc, gec &p, bool neg) {
 #ifndef RBK_FRESH0
 #define RBK_FRESH0 1
 #endif
+#ifndef RBK_CWAVES
+#define RBK_CWAVES 2   // waves per SIMD of pass 1 over cached (folded) bases
+#endif
 #ifndef RBK_WAVES
 #define RBK_WAVES (RBK_PINGPONG ? 2 : 3)   // waves per SIMD the run reduction is compiled for
 #endif
 template <bool FIRST, int FMT, bool NEGC>
-__global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACHED ? 2 : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
+__global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACHED ? RBK_CWAVES : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         const ge *__restrict__ pin, SegTab T, uint64_t E,
                                                         uint32_t invalid, int cw, uint32_t *__restrict__ kout,
