@@ -42,7 +42,9 @@ sys.path.insert(0, ROOT)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of this run. Without a torchrun environment and N > 1 the bench starts "
+                         "N rank processes itself (one per GPU, RCCL); under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=5)
@@ -60,7 +62,8 @@ def parse():
                          "metric")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
     ap.add_argument("--cpu-procs", type=int, default=0,
-                    help="processes of the all-core CPU leg (default: the host cores this rank may use, at most 16)")
+                    help="processes of the all-core CPU leg (default: the CPUs this job may use: the cgroup CPU "
+                         "quota, else the affinity mask)")
     return ap.parse_args()
 
 
@@ -121,14 +124,48 @@ def _cpu_model():
     return "unknown"
 
 
+def cpu_quota():
+    """CPUs this job may use: the cgroup CPU quota (cgroup v2 cpu.max, v1
+    cfs_quota_us / cfs_period_us) when one is set, else None. On the GPU
+    boxes the affinity mask lists the whole machine while the job's cgroup is
+    granted a share of it."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0 and per > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def job_cpus():
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cpu_quota()
+    return max(1, min(aff, int(quota))) if quota else aff
+
+
+FULL_CPU = os.path.join("profiles", "r02d_cpu_baseline_full.json")
+
+
 def cpu_baseline(leaves, procs):
-    """The CPU oracle (oracle/, a C restatement of dalek/bulletproofs with
-    dalek's algorithms; the reference prover is single-threaded) proving a
-    bounded sample of the same workload family: the config-5 statement with
-    `leaves` Merkle leaves. Two legs: one core, and `procs`
-    independent single-thread provers at once (the host's all-core
-    throughput on independent proofs). The full config-5 size on one core is
-    measured once by scripts/cpu_baseline_full.py (profiles/)."""
+    """The CPU oracle (oracle/: a plain-C restatement of dalek/bulletproofs
+    with dalek's algorithms on 5x51-bit limbs — not dalek's AVX2 backend,
+    Cargo.toml:21; the reference prover is single-threaded, prove.rs:79)
+    proving a bounded sample of the same workload family: the config-5
+    statement with `leaves` Merkle leaves. Two legs: one core,
+    and `procs` independent single-thread provers at once, `procs` = the CPUs
+    this job may use (the host's all-core throughput on independent proofs;
+    more processes than the job's CPU quota would only time-slice). The full
+    config-5 size (N = 2^20) on one core takes ~150 s, so it is measured by
+    scripts/cpu_baseline_full.py and reported here from its record."""
     import subprocess
     q, dt, n = _cpu_sample(leaves)
     N = 1
@@ -140,13 +177,29 @@ def cpu_baseline(leaves, procs):
     res = [json.loads(p.communicate()[0]) for p in ps]
     wall = time.perf_counter() - t0
     allcore = sum(r["q"] / r["s"] for r in res)
-    return {"value": round(q / dt, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
-            "sample": "oracle/ C restatement (dalek algorithms, 5x51-bit limbs, 1 thread) proving the config-5 "
-                      "family with %d Merkle leaves: n=%d, N=2^%d, q=%d, warm generators, %.1f s" %
-                      (leaves, n, N.bit_length() - 1, q, dt),
-            "all_cores": {"value": round(allcore, 1), "cores": procs, "wall_s": round(wall, 1),
-                          "sample": "%d independent single-thread oracle provers of the same sample at once" % procs},
-            "host": {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": _cpu_model()}}
+    quota = cpu_quota()
+    aff = len(os.sched_getaffinity(0))
+    out = {"value": round(q / dt, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
+           "sample": "oracle/ plain-C restatement (dalek's algorithms, 5x51-bit limbs, not dalek's AVX2 backend; "
+                     "1 thread like the reference prover) proving the config-5 family with %d Merkle leaves: n=%d, "
+                     "N=2^%d, q=%d, warm generators, %.1f s" % (leaves, n, N.bit_length() - 1, q, dt),
+           "all_cores": {"value": round(allcore, 1), "cores": procs, "wall_s": round(wall, 1),
+                         "per_core": round(allcore / procs, 1),
+                         "sample": "%d independent single-thread oracle provers of the same sample at once" % procs,
+                         "cap": ("the job's cgroup CPU quota (%.1f CPUs) of the %d CPUs in the affinity mask: more "
+                                 "provers than that only time-slice" % (quota, aff)) if quota and procs < aff else
+                                "all CPUs in the affinity mask",
+                         "whole_host_extrapolated": round(allcore / procs * (os.cpu_count() or procs), 1)},
+           "host": {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota, "model": _cpu_model()}}
+    try:
+        full = json.load(open(os.path.join(ROOT, FULL_CPU)))
+        out["full_size_single_core"] = {"value": full["constraints_per_s_warm"], "cold_value":
+                                        full["constraints_per_s_cold"], "n": full["n"], "q": full["q"],
+                                        "N": "2^20", "warm_s": full["warm_s"], "model": full["cpu_model"],
+                                        "source": FULL_CPU + " (scripts/cpu_baseline_full.py on a GPU box)"}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def heartbeat(period=20.0):
@@ -162,16 +215,77 @@ def heartbeat(period=20.0):
     threading.Thread(target=run, daemon=True).start()
 
 
+DIST_INFO = None
+
+
+def dist_info(torch, dist, D, dev, world):
+    """What the ranks saw: the process group's world size and backend, and
+    every rank's HIP device index and PCI bus (gathered over the group)."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bus = "%s" % getattr(p, "pci_bus_id", "?")
+        name = p.name
+    except Exception:
+        bus, name = "?", "?"
+    mine = ("%d:%s" % (dev, bus)).encode()[:30].ljust(30, b" ")
+    ranks = [m.decode().strip() for m in D.all_gather_bytes(mine)] if dist is not None else [mine.decode().strip()]
+    return {"world_size": dist.get_world_size() if dist is not None else 1,
+            "backend": dist.get_backend() if dist is not None else "none (1 rank)",
+            "rank_devices": ranks, "device_name": name,
+            "launcher": "bench.py --gpus" if os.environ.get("BENCH_SPAWNED") else
+                        ("torchrun" if world > 1 else "single process")}
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a torchrun environment: start N rank
+    processes (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on 127.0.0.1), one
+    per GPU, and exit with their status. This process has not touched HIP
+    (nothing here imports torch), so no GPU state is forked or replaced."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in procs:   # a failed rank would leave the others in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     if len(sys.argv) == 3 and sys.argv[1] == "--cpu-sample-child":
         q, dt, _ = _cpu_sample(int(sys.argv[2]))
         print(json.dumps({"q": q, "s": dt}))
         return
     a = parse()
-    heartbeat()
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus is not None and a.gpus != world:
+        sys.exit("bench: --gpus %d but the launcher started %d ranks (WORLD_SIZE)" % (a.gpus, world))
+    if os.environ.get("BENCH_RANK_PROBE"):   # tests/test_host.py: the launcher's view of a rank, no GPU touched
+        print(json.dumps({"rank": rank, "world": world, "local": local, "master": os.environ.get("MASTER_ADDR"),
+                          "spawned": os.environ.get("BENCH_SPAWNED") == "1"}), flush=True)
+        return
+    if rank == 0:
+        heartbeat()
     import torch
     dist = None
     ndev = torch.cuda.device_count()
@@ -191,7 +305,9 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "bulletproof-gadgets_amd"))
     import dist as D
     bpg.lib().bpg_set_device(dev)
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+    global DIST_INFO
+    DIST_INFO = dist_info(torch, dist, D, dev, world)
+    ncpu = job_cpus()
     # consumers mostly sleep on the device (event polls), so 24 threads keep
     # ~9 host cores busy: 8 RNG producers + 16 streams
     per_rank = ncpu // max(world, 1) if world > 1 else ncpu
@@ -354,10 +470,10 @@ def main():
                                     "generators_from_disk_cache": setup["gens_from_cache"]},
         "phase_ms_single_proof": single_phases,
         "roofline": roof,
+        "dist": DIST_INFO,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8
-        out["cpu_baseline"] = cpu_baseline(a.cpu_leaves, a.cpu_procs or max(1, min(16, aff)))
+        out["cpu_baseline"] = cpu_baseline(a.cpu_leaves, a.cpu_procs or job_cpus())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -416,6 +532,7 @@ def bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropie
                    "parallelism": "independent verifications per GPU (%d ranks)" % world},
         "proofs_per_s": round(total / dt, 2),
         "latency_ms_single_verify": round(single_ms, 2),
+        "dist": DIST_INFO,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -435,11 +552,14 @@ def bench_verify_sharded(a, bpg, ctx, syn, prep, D, dist, rank, world, q, n, N, 
     if dist is not None:   # every rank verifies rank 0's bytes
         proof = D.all_gather_bytes(proof)[0]
     V = _commitments(ctx, syn)
+    # every rank prepares the circuit once (bpg_prepare_verifier); per proof:
+    # transcript replay, this rank's slice of the mega-MSM, one 33-byte gather
+    vprep = ctx.prepare(syn.view, verifier=True)
 
-    def verify(p):   # one rank: the unsharded verifier (no process group)
+    def verify(p):   # one rank: the whole mega-MSM, no exchange
         if dist is None:
-            return ctx.r1cs_verify(b"bench", syn.view, V, p)
-        return D.sharded_verify(bpg, ctx, b"bench", syn.view, V, p)
+            return vprep.verify_one(b"bench", V, p)
+        return D.sharded_verify_prepared(bpg, vprep, b"bench", V, p)
 
     def barrier():
         if dist is not None:
@@ -471,6 +591,7 @@ def bench_verify_sharded(a, bpg, ctx, syn, prep, D, dist, rank, world, q, n, N, 
         "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
                    "parallelism": "one verification's mega-MSM split over %d ranks" % world},
         "latency_ms_verify": round(dt / a.steps * 1e3, 3),
+        "dist": DIST_INFO,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -525,6 +646,7 @@ def bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W):
                    "parallelism": "one proof sharded over %d ranks (lanes i = j*%d + rank)" % (world, world)},
         "latency_ms": round(dt / a.steps * 1e3, 1), "phase_ms_last_proof_rank0": phases,
         "prepare_ms": round(prepare_ms, 1),
+        "dist": DIST_INFO,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -542,7 +664,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
     statements; value = statements x q / wall time."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
-    threads = a.threads or 16
+    threads = a.threads or max(2, min(64, job_cpus() // max(world, 1)))   # synthesis is host work: one per CPU
     batch = a.batch or 2 * threads
     texts = [W.config5(50000 + 100003 * rank + i) for i in range(batch * (a.steps + a.warmup))]
     q = bpg.Synth(*texts[0]).q
@@ -581,6 +703,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         "config": {"workload": W.NAMES[5], "q_constraints": q, "statements_per_step_per_gpu": batch,
                    "host_threads_per_gpu": threads},
         "statements_per_s": round(n_st / dt, 2),
+        "dist": DIST_INFO,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

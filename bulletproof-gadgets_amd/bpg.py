@@ -31,7 +31,7 @@ EXPORTS = [
     "bpg_ctx_set_fold_pairs", "bpg_ctx_set_ipp_tail", "bpg_ctx_setup_stats", "bpg_r1cs_prove_sharded", "bpg_cs_create", "bpg_cs_free",
     "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
-    "bpg_prove_prepared",
+    "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -119,6 +119,9 @@ def lib():
         L.bpg_prepare_shard.restype = vp
         L.bpg_prepare_shard.argtypes = [vp, vp, u32, u32]
         L.bpg_prove_prepared.argtypes = [vp, vp, sz, vp, ALLGATHER_FN, vp, vp, sz, ctypes.POINTER(sz)]
+        L.bpg_verify_prepared.argtypes = [vp, vp, sz, vp, vp, sz, vp, u32, u32, vp]
+        L.bpg_ctx_trim.restype = ctypes.c_int64
+        L.bpg_ctx_trim.argtypes = [vp]
         L.bpg_cs_create.restype = vp
         L.bpg_cs_create.argtypes = [ctypes.c_int]
         L.bpg_cs_free.argtypes = [vp]
@@ -340,9 +343,18 @@ class Context:
             raise BpgError("bad strategy")
 
     def setup_stats(self):
-        arr = (ctypes.c_double * 4)()
-        lib().bpg_ctx_setup_stats(self.h, arr, 4)
-        return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2]), "comb_alloc_ms": arr[3]}
+        arr = (ctypes.c_double * 5)()
+        lib().bpg_ctx_setup_stats(self.h, arr, 5)
+        return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2]), "comb_alloc_ms": arr[3],
+                "comb_bytes": arr[4]}
+
+    def trim(self):
+        """bpg_ctx_trim: drop cached comb tables / generator slices no proof
+        holds; returns the table bytes released."""
+        r = lib().bpg_ctx_trim(self.h)
+        if r < 0:
+            raise BpgError(last_error())
+        return r
 
     def msm(self, scalars, points):
         out = ctypes.create_string_buffer(32)
@@ -428,7 +440,10 @@ def _allgather_cb(allgather, world):
 
     def cb(_user, send, nbytes, recv):
         try:
-            parts = allgather(ctypes.string_at(send, nbytes))
+            parts = list(allgather(ctypes.string_at(send, nbytes)))
+            if len(parts) != world or any(len(p) != nbytes for p in parts):
+                raise BpgError("all-gather returned %d parts of %s bytes, want %d x %d"
+                               % (len(parts), sorted({len(p) for p in parts}), world, nbytes))
             ctypes.memmove(recv, b"".join(parts), nbytes * world)
             return 0
         except Exception as e:  # the library turns a failed exchange into an error status
@@ -478,6 +493,18 @@ class Prepared:
         if rc != 0:
             raise BpgError(last_error())
         return [res[k] == 1 for k in range(count)]
+
+    def verify_one(self, label, V, proof, entropy=b"\x05" * 32, shard=0, nshards=1):
+        """bpg_verify_prepared on a verifier-prepared circuit: nshards == 1
+        -> bool verdict; else -> (ok, 32-byte partial) of shard `shard`."""
+        if isinstance(V, (list, tuple)):
+            V = b"".join(V)
+        part = ctypes.create_string_buffer(32)
+        rc = lib().bpg_verify_prepared(self.h, label, len(label), V or b"\0" * 32, proof, len(proof), entropy,
+                                       shard, nshards, part)
+        if rc < 0:
+            raise BpgError(last_error())
+        return rc == 1 if nshards == 1 else (rc == 1, part.raw)
 
     def __del__(self):
         try:

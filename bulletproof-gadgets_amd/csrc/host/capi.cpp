@@ -159,9 +159,28 @@ int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
     if (!ctx) return -1;
     DeviceContext &c = DeviceContext::get(ctx->device);
     std::lock_guard<std::mutex> lk(c.mu);
-    const double v[4] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms};
-    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
+    double resident = 0;
+    for (auto &e : c.combs) resident += (double)e.second->bytes;
+    const double v[5] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms, resident};
+    for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
     return 0;
+}
+int64_t bpg_ctx_trim(bpg_ctx *ctx) {
+    return guarded([&]() -> int64_t {
+        if (!ctx) throw std::runtime_error("NULL context");
+        DeviceContext &c = DeviceContext::get(ctx->device);
+        std::lock_guard<std::mutex> lk(c.mu);
+        int64_t freed = 0;
+        for (auto e = c.combs.begin(); e != c.combs.end();) {
+            if (e->second.use_count() == 1) { freed += (int64_t)e->second->bytes; e = c.combs.erase(e); }
+            else ++e;
+        }
+        for (auto e = c.slices.begin(); e != c.slices.end();) {
+            if (e->second.use_count() == 1) e = c.slices.erase(e);
+            else ++e;
+        }
+        return freed;
+    }, (int64_t)-1);
 }
 
 int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity) {
@@ -265,6 +284,18 @@ bpg_prepared *bpg_prepare_verifier(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
     return bpg_prepare(ctx, &v);
 }
 void bpg_prepared_free(bpg_prepared *p) { delete p; }
+int bpg_verify_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len, const uint8_t *V, const uint8_t *proof,
+                        size_t proof_len, const uint8_t entropy[32], uint32_t shard, uint32_t nshards,
+                        uint8_t *partial) {
+    return guarded([&]() -> int {
+        if (!p || !label || !entropy || (!proof && proof_len)) throw std::runtime_error("NULL argument");
+        const PreparedCS &cs = *p->p;
+        if (cs.prover) throw std::runtime_error("circuit prepared for proving: use bpg_prepare_verifier");
+        if (!V && cs.m) throw std::runtime_error("NULL commitments");
+        if (nshards > 1 && !partial) throw std::runtime_error("NULL partial");
+        return gpu_verify_shard(cs, label, label_len, V, proof, proof_len, entropy, shard, nshards, partial);
+    }, -1);
+}
 bpg_prepared *bpg_prepare_shard(bpg_ctx *ctx, const bpg_r1cs_view *cs, uint32_t rank, uint32_t world) {
     return guarded([&]() -> bpg_prepared * {
         if (!cs->a_L) throw std::runtime_error("prover view without witness");

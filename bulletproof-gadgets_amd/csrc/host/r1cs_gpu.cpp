@@ -5,7 +5,9 @@
 // and src/r1cs/proof.rs `to_bytes` / `from_bytes`.
 #include "r1cs_gpu.h"
 
+#include <fcntl.h>
 #include <stdlib.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -147,22 +149,43 @@ static bool gens_cache_check(const std::vector<dev::NielsD> &G, const std::vecto
     return true;
 }
 
-std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uint32_t world) {
+// A cache file is read only if nobody but this user could have written it:
+// a regular file owned by the effective uid, not writable by group or others,
+// in a directory owned by this uid (or root) that group and others cannot
+// write either. The verifier never uses a loaded set (DeviceContext::gens).
+static bool gens_cache_trusted(const std::string &dir, int fd) {
+    struct stat fs, ds;
+    if (fstat(fd, &fs) != 0 || stat(dir.c_str(), &ds) != 0) return false;
+    const uid_t me = geteuid();
+    if (!S_ISREG(fs.st_mode) || fs.st_uid != me || (fs.st_mode & (S_IWGRP | S_IWOTH))) return false;
+    if (!S_ISDIR(ds.st_mode) || (ds.st_uid != me && ds.st_uid != 0) || (ds.st_mode & (S_IWGRP | S_IWOTH))) return false;
+    return true;
+}
+
+std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uint32_t world, bool verifier) {
     if (world < 1 || rank >= world || N % world) throw std::runtime_error("bad generator slice");
     std::lock_guard<std::mutex> lk(mu);
     BPG_HIP(hipSetDevice(device));
-    if (!full || full->N < N) {
+    // a set loaded from the on-disk cache is checked only by a checksum and
+    // its first points: the verifier's soundness must not rest on a file, so
+    // a verifier request re-derives it (once) from the SHAKE256 chains
+    if (!full || full->N < N || (verifier && gens_from_cache)) {
         const double t0 = now_ms();
-        const uint32_t cap = std::max<uint32_t>(N, 64);
+        const uint32_t cap = std::max<uint32_t>(std::max<uint32_t>(N, 64), full ? full->N : 0);
         std::shared_ptr<GenSet> gs(new GenSet());
         gs->device = device;
         gs->N = cap;
         BPG_HIP(hipMalloc(&gs->G, 2 * (size_t)cap * sizeof(dev::NielsD)));
         BPG_HIP(hipMalloc(&gs->H, 2 * (size_t)cap * sizeof(dev::NielsD)));
-        const std::string dir = gens_cache_dir();
+        const std::string dir = verifier ? std::string() : gens_cache_dir();
         bool loaded = false;
         if (!dir.empty()) {
-            if (FILE *f = fopen(gens_cache_path(dir, cap).c_str(), "rb")) {
+            FILE *f = fopen(gens_cache_path(dir, cap).c_str(), "rb");
+            if (f && !gens_cache_trusted(dir, fileno(f))) {
+                fclose(f);
+                f = nullptr;
+            }
+            if (f) {
                 uint64_t hdr[3] = {0, 0, 0};
                 std::vector<dev::NielsD> hG(cap), hH(cap);
                 if (fread(hdr, 8, 3, f) == 3 && hdr[0] == GENS_MAGIC && hdr[1] == cap &&
@@ -188,13 +211,15 @@ std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uin
             }
             BPG_HIP(hipDeviceSynchronize());
             (void)hipFree(duni);
-            if (!dir.empty()) {   // write-then-rename: concurrent processes never read a partial file
+            const std::string wdir = gens_cache_dir();
+            if (!wdir.empty()) {   // write-then-rename: concurrent processes never read a partial file
                 std::vector<dev::NielsD> hG(cap), hH(cap);
                 BPG_HIP(hipMemcpy(hG.data(), gs->G, (size_t)cap * sizeof(dev::NielsD), hipMemcpyDeviceToHost));
                 BPG_HIP(hipMemcpy(hH.data(), gs->H, (size_t)cap * sizeof(dev::NielsD), hipMemcpyDeviceToHost));
-                const std::string path = gens_cache_path(dir, cap);
+                const std::string path = gens_cache_path(wdir, cap);
                 const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
-                if (FILE *f = fopen(tmp.c_str(), "wb")) {
+                const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0644);
+                if (FILE *f = fd >= 0 ? fdopen(fd, "wb") : nullptr) {
                     const uint64_t hdr[3] = {GENS_MAGIC, cap, gens_checksum(hG, hH)};
                     bool ok = fwrite(hdr, 8, 3, f) == 3 && fwrite(hG.data(), sizeof(dev::NielsD), cap, f) == cap &&
                               fwrite(hH.data(), sizeof(dev::NielsD), cap, f) == cap;
@@ -206,6 +231,10 @@ std::shared_ptr<const GenSet> DeviceContext::gens(uint32_t N, uint32_t rank, uin
         launch_niels_neg(gs->G, gs->G + cap, cap, 0);
         launch_niels_neg(gs->H, gs->H + cap, cap, 0);
         BPG_HIP(hipDeviceSynchronize());
+        if (full && gens_from_cache) {   // slices / tables of the loaded set: rebuilt from the derived one
+            slices.clear();
+            combs.clear();
+        }
         full = gs;
         gens_from_cache = loaded;
         gens_ms += now_ms() - t0;
@@ -612,13 +641,40 @@ static Transcript prover_transcript(const PreparedCS &cs, const uint8_t *label, 
 // blindings, s_L[n], s_R[n], then the t_1, t_3..t_6 blindings. The RNG is
 // forked from the transcript before any challenge, so all draws can be made
 // before the device work starts. Up to 8 proofs run in lockstep (Strobe8).
+// The producers' host-to-device copies (95 MB per 2^20 proof, a few GB/s in
+// all) go to BPG_PRODUCER_STREAMS streams per device shared by all producer
+// threads (default 1; 0: one stream per producer thread). Every HIP stream
+// takes one of the process's GPU_MAX_HW_QUEUES hardware queues, and streams
+// beyond that share queues in order, so a consumer stream that shared a
+// queue with a producer waited behind its copies (and the copies behind its
+// kernels).
+static hipStream_t shared_producer_stream(int device, int nstreams) {
+    static std::mutex mu;
+    static std::map<int, std::vector<hipStream_t>> streams;
+    static std::map<int, unsigned> next;
+    std::lock_guard<std::mutex> lk(mu);
+    std::vector<hipStream_t> &v = streams[device];
+    if ((int)v.size() < nstreams) {
+        hipStream_t s;
+        BPG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        v.push_back(s);
+        return s;
+    }
+    return v[next[device]++ % v.size()];
+}
 ProducerStage &producer_stage(int device) {
     static thread_local std::map<int, std::unique_ptr<ProducerStage>> m;
+    static const int nshared = [] { const char *e = getenv("BPG_PRODUCER_STREAMS"); return e ? atoi(e) : 1; }();
     auto &p = m[device];
     if (!p) {
         BPG_HIP(hipSetDevice(device));
         p.reset(new ProducerStage());
-        BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+        if (nshared > 0) {
+            p->st = shared_producer_stream(device, nshared);
+            p->owns_stream = false;
+        } else {
+            BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+        }
         for (int b = 0; b < 2; b++) {
             BPG_HIP(hipHostMalloc((void **)&p->host[b], (size_t)8 * ProducerStage::CHUNK * 64, hipHostMallocDefault));
             BPG_HIP(hipEventCreateWithFlags(&p->ev[b], hipEventBlockingSync | hipEventDisableTiming));
@@ -633,7 +689,7 @@ ProducerStage::~ProducerStage() {
         if (host[b]) (void)hipHostFree(host[b]);
         if (ev[b]) (void)hipEventDestroy(ev[b]);
     }
-    if (st) (void)hipStreamDestroy(st);
+    if (st && owns_stream) (void)hipStreamDestroy(st);
 }
 
 void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
@@ -952,7 +1008,7 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     // level-k points, and after the group's last round one pass builds the
     // next level from level k: comb tables from the level-0 generators (a
     // pair), else the three- (pair) or seven-scalar (triple) Straus fold.
-    const int group_cfg = sharded ? std::min(cs.strat.group(), 2) : cs.strat.group();
+    const int group_cfg = cs.strat.group();
     Scalar rho_h[2][4];   // the pending rounds' fold scalars (G a/b, H a/b), oldest first
     int depth = 0;        // pending levels: Ghat at level k, this round at level k + depth
     int cur = -1;      // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
@@ -961,7 +1017,10 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     // folding them (each fold there is a latency-bound launch). The sharded
     // prover always ends in the tail: its last local round's fold is needed
     // (as weights) for the final generator of each rank.
-    const uint32_t tail_len = cs.strat.tail();
+    // sharded: the materialised levels are Nl/8^j (or /4^j, /2^j) after the
+    // first group, so the last one of at least 2 lanes has at most 8: a
+    // threshold of 8 or more always meets it
+    const uint32_t tail_len = sharded ? std::max<uint32_t>(cs.strat.tail(), 8u) : cs.strat.tail();
     bool tail = false;
     uint32_t M = 0;
     uint32_t len = Nl;
@@ -1309,7 +1368,7 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     if (lgn >= 32) return 0;
     if (!Scalar::from_canonical(ipp + 64 * lgn, pa) || !Scalar::from_canonical(ipp + 64 * lgn + 32, pb)) return 0;
     if (N != (1u << lgn)) return 0;
-    std::shared_ptr<const GenSet> gs = ctx.gens(N);
+    std::shared_ptr<const GenSet> gs = ctx.gens(N, 0, 1, true);
     Workspace &ws = thread_workspace(cs.device);
     hipStream_t st = ws.st;
     ws.tabs.grow(8 * 40 * sizeof(ScD));

@@ -38,7 +38,8 @@ struct GenSet {
     ~GenSet();
 };
 // Comb tables of a generator set for the IPP's first two rounds:
-// points j in [N/4, N) of G and of H, 512 packed affine-Niels entries each.
+// points j in [N/4, N) of G and of H, COMB_WIN x COMB_ENT (43 x 32 at the
+// default COMB_BITS 6) packed affine-Niels entries of 96 B each.
 struct CombTables {
     int device = 0;
     uint32_t N = 0;
@@ -76,7 +77,8 @@ struct DeviceContext {
     static DeviceContext &get(int device);
     // Thread-safe. world == 1: a full set with at least N points (grown on
     // demand); else the N / world points of rank `rank` of BulletproofGens(N).
-    std::shared_ptr<const GenSet> gens(uint32_t N, uint32_t rank = 0, uint32_t world = 1);
+    // verifier: never a set loaded from the on-disk cache (re-derived once).
+    std::shared_ptr<const GenSet> gens(uint32_t N, uint32_t rank = 0, uint32_t world = 1, bool verifier = false);
     // Comb tables over the first N points of `gs`, built on first use and
     // cached per (N, slice); null when N < 8 or when they would not fit in
     // free HBM (tables not in use are evicted first).
@@ -130,7 +132,8 @@ struct RngBlock {
 // Per-thread staging of RNG output into device buffers.
 struct ProducerStage {
     static const uint32_t CHUNK = 2048;   // draws per staged chunk
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;                 // shared by producer threads unless owns_stream
+    bool owns_stream = true;
     uint8_t *host[2] = {nullptr, nullptr};   // pinned, 8 x CHUNK x 64 B each
     hipEvent_t ev[2] = {nullptr, nullptr};
     ~ProducerStage();

@@ -543,7 +543,11 @@ static bool is_instance(const std::string &t) { return t.size() >= 2 && t[0] == 
 
 // gadget_grammar.lalrpop:46-72 (Tree)
 struct Tree { std::vector<std::string> inst, wit; std::unique_ptr<Pattern> p; };
-static Tree parse_tree(const std::vector<std::string> &t, size_t &pos) {
+// Nesting bound of the recursive pattern parsers (a deeper text would only
+// overflow the stack; the crate's own circuits nest at most 32 deep).
+static const int MAX_PATTERN_DEPTH = 512;
+static Tree parse_tree(const std::vector<std::string> &t, size_t &pos, int depth = 0) {
+    if (depth > MAX_PATTERN_DEPTH) throw StatementError("MERKLE tree nested too deeply");
     if (pos >= t.size() || t[pos] != "(") throw StatementError("malformed MERKLE tree");
     pos++;
     Tree out;
@@ -552,7 +556,7 @@ static Tree parse_tree(const std::vector<std::string> &t, size_t &pos) {
         if (pos >= t.size()) throw StatementError("malformed MERKLE tree");
         std::unique_ptr<Pattern> sub;
         if (t[pos] == "(") {
-            Tree s = parse_tree(t, pos);
+            Tree s = parse_tree(t, pos, depth + 1);
             out.inst.insert(out.inst.end(), s.inst.begin(), s.inst.end());
             out.wit.insert(out.wit.end(), s.wit.begin(), s.wit.end());
             sub = std::move(s.p);
@@ -573,7 +577,8 @@ static Tree parse_tree(const std::vector<std::string> &t, size_t &pos) {
 // ------------------------------------------- Gadget-API entry points
 // Pattern in the reference's Display form (merkle_tree_gadget.rs:21-29):
 // "W", "I" or "H(<left> <right>)".
-static std::unique_ptr<Pattern> parse_display_pattern(const std::string &s, size_t &pos) {
+static std::unique_ptr<Pattern> parse_display_pattern(const std::string &s, size_t &pos, int depth = 0) {
+    if (depth > MAX_PATTERN_DEPTH) throw StatementError("pattern nested too deeply");
     while (pos < s.size() && s[pos] == ' ') pos++;
     if (pos >= s.size()) throw StatementError("malformed pattern");
     const char c = s[pos++];
@@ -581,8 +586,8 @@ static std::unique_ptr<Pattern> parse_display_pattern(const std::string &s, size
     if (c != 'H' || pos >= s.size() || s[pos] != '(') throw StatementError("malformed pattern");
     pos++;
     std::unique_ptr<Pattern> p(new Pattern{'H', nullptr, nullptr});
-    p->l = parse_display_pattern(s, pos);
-    p->r = parse_display_pattern(s, pos);
+    p->l = parse_display_pattern(s, pos, depth + 1);
+    p->r = parse_display_pattern(s, pos, depth + 1);
     while (pos < s.size() && s[pos] == ' ') pos++;
     if (pos >= s.size() || s[pos] != ')') throw StatementError("malformed pattern");
     pos++;
@@ -594,6 +599,20 @@ void merkle_tree_assemble(ConstraintSystem &cs, const LC &root, std::vector<LC> 
     std::unique_ptr<Pattern> p = parse_display_pattern(pattern, pos);
     while (pos < pattern.size() && pattern[pos] == ' ') pos++;
     if (pos != pattern.size()) throw StatementError("malformed pattern");
+    // merkle_parse emits constraints as it goes: refuse a pattern with more
+    // leaves than variables before it starts, so a failing call leaves the
+    // recorder unchanged
+    size_t nw = 0, ni = 0;
+    std::vector<const Pattern *> stack{p.get()};
+    while (!stack.empty()) {
+        const Pattern *q = stack.back();
+        stack.pop_back();
+        if (q->kind == 'W') nw++;
+        else if (q->kind == 'I') ni++;
+        else { stack.push_back(q->l.get()); stack.push_back(q->r.get()); }
+    }
+    if (nw > wit.size() || ni > inst.size())
+        throw StatementError("too few variables provided to satisfy the given pattern");
     LC h = merkle_parse(cs, wit, inst, *p);
     cs.constrain(h - root);
 }

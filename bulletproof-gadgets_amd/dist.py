@@ -63,6 +63,17 @@ def sharded_prove(ctx, label, view, entropy):
     return ctx.r1cs_prove_sharded(label, view, entropy, rank, world, all_gather_bytes)
 
 
+def sharded_verify_prepared(bpg, prep, label, V, proof, entropy=b"\x05" * 32):
+    """The same over a circuit every rank prepared once (ctx.prepare(view,
+    verifier=True)): per proof only the transcript replay, the device work of
+    this rank's slice and one all-gather of 33 bytes."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if world == 1:
+        return prep.verify_one(label, V, proof, entropy)
+    ok, part = prep.verify_one(label, V, proof, entropy, rank, world)
+    return combine_verify(bpg, all_gather_bytes(bytes([1 if ok else 0]) + part))
+
+
 def sharded_verify(bpg, ctx, label, view, V, proof, entropy=b"\x05" * 32):
     """Verifier::verify (verify.rs:71) with its mega-MSM split over all ranks
     of the default process group; every rank returns the same verdict."""

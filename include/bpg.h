@@ -136,30 +136,40 @@ void bpg_ctx_destroy(bpg_ctx *ctx);
 /* IPP fold strategy of the calls made through `ctx` (bpg_r1cs_prove,
  * bpg_prepare; a prepared circuit keeps the strategy it was prepared with).
  * Proof bytes are identical under every strategy.
- *   fold_tables 1: comb tables of the generators (HBM-resident, ~117 KB x N
- *     per device) fold IPP rounds 0-1 in one table pass; 0: per-round
- *     variable-base fold; -1 (default): on unless env BPG_FOLD_TABLES=0
- *     (tables are skipped when they do not fit in free HBM).
+ *   fold_tables 1: comb tables of the generators fold IPP rounds 0-1 in one
+ *     table pass; 0: per-round variable-base fold; -1 (default): on unless
+ *     env BPG_FOLD_TABLES=0 (tables are skipped when they do not fit in free
+ *     HBM). Footprint (default build, COMB_BITS 6): generators j in [N/4, N)
+ *     of G and of H, COMB_WIN (43) windows x COMB_ENT (32) entries x 96 B
+ *     each, i.e. 0.75 x 43 x 32 x 96 x 2 B = ~198 KB x N per device
+ *     (208 GB at N = 2^20; a sharded rank holds the tables of its N/world
+ *     generators).
  *   fold_pairs 2: after the comb pass, rounds k, k+1, k+2 fold together
  *     (level k+3 from level k by a seven-scalar Straus pass; rounds k+1, k+2
  *     expand their bases into level-k points); 1: rounds fold in pairs
  *     (three-scalar Straus pass); 0: one fold per round; -1 (default): 2,
  *     or 1 with env BPG_FOLD_TRIPLES=0, or 0 with env BPG_FOLD_PAIRS=0. The
- *     sharded prover folds at most in pairs. */
+ *     sharded prover uses the same grouping. */
 int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode);
 int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
 /* IPP tail threshold of `ctx`'s calls: once a materialised generator level
  * has at most `lanes` points, the remaining rounds weight its points instead
  * of folding them (-1, the default: env BPG_IPP_TAIL, else 4096). Proof bytes
  * are identical for every threshold; small values exercise the fold passes on
- * small circuits. */
+ * small circuits. The sharded prover must end its local rounds in the tail
+ * and uses max(lanes, 8). */
 int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes);
 
 /* Cold-setup breakdown of the device `ctx` is on: out[0] ms spent deriving
  * (or loading) generators, out[1] ms building comb tables, out[2] 1 if the
  * generators came from the on-disk cache, out[3] ms of out[1] spent
- * allocating the tables' memory. */
+ * allocating the tables' memory, out[4] bytes of comb tables resident. */
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n);
+/* Release the device's cached comb tables and sharded generator slices that
+ * no proof in flight holds (they are rebuilt on next use): lets another
+ * process or circuit size on the same GPU have the HBM. Returns the bytes of
+ * comb tables released, < 0 on error. */
+int64_t bpg_ctx_trim(bpg_ctx *ctx);
 
 /* Ensure G_i, H_i for i < capacity are resident (BulletproofGens::new(cap,1),
  * bulletproofs@2.1.0 generators.rs). */
@@ -232,9 +242,21 @@ int bpg_r1cs_verify_shard(bpg_ctx *ctx, const uint8_t *label, size_t label_len,
  * 32 zero bytes). Returns 0, or -1 if an input does not decompress. */
 int bpg_point_sum(const uint8_t *points, uint32_t count, uint8_t out[32]);
 
+/* Verifier::verify (verify.rs:71) of one proof against a circuit prepared by
+ * bpg_prepare_verifier (constraint matrix already resident: no per-call
+ * transposition or upload), on the calling thread. nshards == 1: returns
+ * 1 accept / 0 reject (`partial` may be NULL). nshards > 1: shard `shard` of
+ * the mega-MSM exactly as bpg_r1cs_verify_shard (1 partial written, 0
+ * rejected). < 0 on error. Every rank of a sharded verification prepares the
+ * whole circuit once and then exchanges one 32-byte partial per proof. */
+typedef struct bpg_prepared bpg_prepared;
+int bpg_verify_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len,
+                        const uint8_t *V, const uint8_t *proof, size_t proof_len,
+                        const uint8_t entropy[32], uint32_t shard, uint32_t nshards,
+                        uint8_t *partial);
+
 /* Prepared (HBM-resident) circuit for repeated proving: uploads a_L/a_R/a_O
  * and the transposed constraint matrix once. */
-typedef struct bpg_prepared bpg_prepared;
 bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs);
 void bpg_prepared_free(bpg_prepared *p);
 /* The same for verification only (witness fields of `cs` ignored): the

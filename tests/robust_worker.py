@@ -18,8 +18,12 @@ def main():
         bpg.set_seed(5)
         syn = bpg.Synth(*W.config3())
         ctx = bpg.Context(0)
-        proof, _ = ctx.r1cs_prove(b"cache", syn.view, bytes(32))
-        print(json.dumps({"proof": proof.hex(), **ctx.setup_stats()}))
+        proof, V = ctx.r1cs_prove(b"cache", syn.view, bytes(32))
+        st = ctx.setup_stats()
+        # the verifier never uses a set loaded from the file: it re-derives
+        ok = ctx.r1cs_verify(b"cache", syn.view, V, proof)
+        print(json.dumps({"proof": proof.hex(), **st, "verified": ok,
+                          "from_cache_after_verify": ctx.setup_stats()["gens_from_cache"]}))
     else:
         # two circuit sizes proved at once from two threads on a fresh device
         # context: the larger one grows the generator set while the smaller

@@ -1,9 +1,15 @@
-"""World-size-2 tests of the multi-GPU plumbing on the CPU (gloo backend):
-the exchange used by the sharded verifier (all-gather of 33-byte messages,
-host Ristretto point sum in libbpg) and the bench's max-over-ranks timing.
-Partials are computed by the CPU oracle here (no GPU): rank r sums its slice
-of one MSM; the gathered partials must add up to the oracle's full MSM, and
-a verdict is an identity check over them (dist.combine_verify)."""
+"""Tests of the multi-GPU plumbing (dist.py).
+
+CPU (gloo, world size 2): the exchange used by the sharded verifier
+(all-gather of 33-byte messages, host Ristretto point sum in libbpg) and the
+bench's max-over-ranks timing. Without a GPU the partials come from the CPU
+oracle: rank r sums its slice of one MSM; the gathered partials must add up to
+the oracle's full MSM, and a verdict is an identity check over them
+(dist.combine_verify).
+
+GPU (-m gpu): the same exchange with the product's own partials
+(bpg_verify_prepared) over gloo at world size 2, and the RCCL ("nccl")
+process group bench.py uses, at world size 1 (tests/dist_worker.py)."""
 import os
 import random
 import socket
@@ -66,3 +72,49 @@ def test_gloo_world2_sharded_exchange(tmp_path):
     for r in range(WORLD):
         res = eval(open(os.path.join(tmp_path, "r%d" % r)).read())
         assert all(res.values()), (r, res)
+
+
+def _run_device_ranks(backend, world, tmp_path):
+    import json
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"), backend,
+                                       str(tmp_path / ("r%d.json" % r))], env=env))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=150))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert rcs == [0] * world, rcs
+    return [json.load(open(tmp_path / ("r%d.json" % r))) for r in range(world)]
+
+
+@pytest.mark.gpu
+def test_nccl_world1_exchange(tmp_path):
+    """The RCCL process group bench.py initialises between GPUs, at world
+    size 1 on cuda:0: the cuda-tensor all-gather and MAX all-reduce of
+    dist.py, and verdicts through dist.sharded_verify(_prepared) and through
+    two shards' product partials combined over the gather."""
+    (res,) = _run_device_ranks("nccl", 1, tmp_path)
+    assert res["backend"] == "nccl" and res["world"] == 1 and res["comm_device"].startswith("cuda")
+    for k in ("gather_ok", "max_ok", "accept", "reject", "accept_per_call", "accept2", "reject2"):
+        assert res[k] is True, (k, res)
+
+
+@pytest.mark.gpu
+def test_gloo_world2_product_partials(tmp_path):
+    """World 2 over gloo with the PRODUCT's shard partials (bpg_verify_prepared
+    on the device, one shard per rank): a valid proof's partials add up to the
+    identity, a tampered proof's do not."""
+    res = _run_device_ranks("gloo", 2, tmp_path)
+    for r in res:
+        assert r["world"] == 2
+        for k in ("gather_ok", "max_ok", "accept", "reject"):
+            assert r[k] is True, (k, r)

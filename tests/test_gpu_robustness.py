@@ -2,7 +2,8 @@
 
 * the on-disk generator cache (bpg_gens_cache_dir): the first process
   derives and writes it, the next one loads it and proves the same bytes; a
-  corrupted file is detected and re-derived;
+  corrupted or group-writable file is not used, and the verifier re-derives
+  the set rather than trusting the file;
 * two circuit sizes proved concurrently from two host threads on a fresh
   context (the larger circuit grows the generator set while the smaller
   circuit's proofs hold their snapshot) give the same bytes as sequential
@@ -39,6 +40,12 @@ def test_generator_disk_cache(tmp_path):
     assert len(files) == 1
     b = run("cache", str(tmp_path))
     assert b["gens_from_cache"] and b["proof"] == a["proof"]
+    # the verifier re-derived instead of trusting the file
+    assert a["verified"] and b["verified"] and not b["from_cache_after_verify"]
+    os.chmod(files[0], 0o664)                        # group-writable: never loaded
+    d = run("cache", str(tmp_path))
+    assert not d["gens_from_cache"] and d["proof"] == a["proof"]
+    os.chmod(files[0], 0o644)
     raw = bytearray(files[0].read_bytes())
     raw[100000] ^= 1
     files[0].write_bytes(bytes(raw))

@@ -100,3 +100,44 @@ def test_product_fails_loudly_without_device(bpg, resources):
         bpg.prove("x", fx["inst"], fx["wtns"], fx["gadgets"])
     assert not bpg.verify("x", fx["inst"], b"\0" * 417, "", fx["gadgets"])
     assert "no HIP device" in bpg.last_error()
+
+
+def _bench(args, **env):
+    import json
+    import subprocess
+    import sys
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=e, capture_output=True,
+                       text=True, timeout=60)
+    return r.returncode, [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")], r.stderr
+
+
+def test_bench_gpus_spawns_ranks():
+    """`bench.py --gpus N` outside torchrun starts N rank processes itself
+    (one per GPU, rendezvous on 127.0.0.1) before anything touches HIP."""
+    rc, lines, err = _bench(["--gpus", "4"], BENCH_RANK_PROBE="1")
+    assert rc == 0, err
+    assert sorted(l["rank"] for l in lines) == [0, 1, 2, 3]
+    assert all(l["world"] == 4 and l["local"] == l["rank"] and l["spawned"] for l in lines)
+    assert all(l["master"] == "127.0.0.1" for l in lines)
+
+
+def test_bench_gpus_mismatch_fails_loudly():
+    rc, _, err = _bench(["--gpus", "8"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", BENCH_RANK_PROBE="1")
+    assert rc != 0 and "--gpus 8" in err
+    rc, lines, _ = _bench(["--gpus", "2"], WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", BENCH_RANK_PROBE="1")
+    assert rc == 0 and lines[0]["world"] == 2 and not lines[0]["spawned"]
+
+
+def test_bench_cpu_share_detection():
+    """The all-core CPU leg sizes itself to the job's CPU share (cgroup quota
+    when set, else the affinity mask) and never above the affinity mask."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    n = b.job_cpus()
+    assert 1 <= n <= len(os.sched_getaffinity(0))
+    q = b.cpu_quota()
+    assert q is None or q > 0
