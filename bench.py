@@ -692,6 +692,18 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
     last = texts[-1]
     if rank == 0 and not bpg.verify("bench", last[0], outs[-1][0], outs[-1][1], last[2]):
         raise SystemExit("bench: a statement's proof failed to verify")
+    # where one statement's time goes, on one otherwise idle thread (outside
+    # the timed region): synthesis, prepare (transpose + upload), prove
+    t0 = time.perf_counter()
+    syn = bpg.Synth(*last)
+    t1 = time.perf_counter()
+    ctx = bpg.Context(torch.cuda.current_device() if torch.cuda.is_available() else 0)
+    prep = ctx.prepare_shard(syn.view, 0, 1)
+    t2 = time.perf_counter()
+    prep.prove_one(b"bench", b"\x03" * 32)
+    t3 = time.perf_counter()
+    phases = {"synthesis_ms": round((t1 - t0) * 1e3, 1), "prepare_ms": round((t2 - t1) * 1e3, 1),
+              "prove_ms": round((t3 - t2) * 1e3, 1), "prove_phases_ms": bpg.last_timings()}
     n_st = batch * a.steps * world
     out = {
         "metric": "R1CS prove constraints/sec end to end over distinct statements (c_prove: parse + synthesis + "
@@ -703,6 +715,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         "config": {"workload": W.NAMES[5], "q_constraints": q, "statements_per_step_per_gpu": batch,
                    "host_threads_per_gpu": threads},
         "statements_per_s": round(n_st / dt, 2),
+        "single_statement_ms": phases,
         "dist": DIST_INFO,
     }
     if rank == 0:

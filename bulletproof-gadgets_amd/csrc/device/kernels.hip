@@ -926,6 +926,117 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
     }
 }
 
+// Window rows in two launches spread over many blocks (ROW_TWO_LEVEL, the
+// default; else k_bucket_seg + k_row_reduce above, one block per row).
+// Row r is cut into SB blocks of B threads, thread t of block beta owning the
+// L buckets [s L, s L + L) of segment s = beta B + t:
+//   A_s = sum_j (j+1) S_{sL+j},  T_s = sum_j S_{sL+j}   (running sum, 2L adds)
+//   R = sum_s A_s + L sum_s s T_s
+//     = sum_beta Bb_beta + B L sum_beta beta U_beta, with
+//   Bb_beta = sum_t A_t + L sum_{t>=1} suf_t,  U_beta = suf_0,
+// suf_t = sum_{u>=t} T_u the block's inclusive suffix scan (sum_t t T_t =
+// sum_{t>=1} suf_t). k_row_blocks writes (Bb, U) per block; k_row_final does
+// the same weighted combine over the SB blocks of a row (one wave per row).
+#ifndef ROW_TWO_LEVEL
+#define ROW_TWO_LEVEL 1
+#endif
+#define ROW_MAX_THREADS 4096   // threads per row (segments of L = half / 4096 buckets at c = 16)
+__global__ __launch_bounds__(256) void k_row_blocks(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
+                                                    uint32_t half, uint32_t L, int lgL, uint32_t SB, uint32_t nmsm,
+                                                    uint32_t W, ge *__restrict__ blkB, ge *__restrict__ blkU,
+                                                    ge *__restrict__ rows_out) {
+    __shared__ ge sh[256];
+    const uint32_t B = blockDim.x, t = threadIdx.x;
+    const uint32_t row = blockIdx.x / SB, beta = blockIdx.x % SB;
+    const size_t b0 = (size_t)row * half + ((size_t)beta * B + t) * L;
+    ge run, acc, p;
+    bucket_load(run, buckets, bflag, b0 + L - 1);
+    acc = run;
+    for (int j = (int)L - 2; j >= 0; j--) {
+        bucket_load(p, buckets, bflag, b0 + j);
+        ge_add(run, run, p);
+        ge_add(acc, acc, run);
+    }
+    // inclusive suffix scan of T (= run) over the block's threads
+    ge_store(&sh[t], run);
+    for (uint32_t d = 1; d < B; d <<= 1) {
+        __syncthreads();
+        ge a, b;
+        const bool act = t + d < B;
+        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
+        __syncthreads();
+        if (act) ge_store(&sh[t], a);
+    }
+    __syncthreads();
+    ge suf;
+    ge_load(suf, &sh[t]);
+    ge U;
+    if (t == 0) U = suf;
+    if (t > 0) {
+        ge_dbl_n(suf, lgL);   // L suf_t
+        ge_add(acc, acc, suf);
+    }
+    __syncthreads();
+    ge_store(&sh[t], acc);
+    for (uint32_t w = B / 2; w >= 1; w >>= 1) {
+        __syncthreads();
+        if (t < w) {
+            ge a, b;
+            ge_load(a, &sh[t]); ge_load(b, &sh[t + w]);
+            ge_add(a, a, b);
+            ge_store(&sh[t], a);
+        }
+    }
+    if (t == 0) {
+        ge r; ge_load(r, &sh[0]);
+        if (SB == 1) {
+            ge_store(rows_out + row_perm(row, nmsm, W), r);
+        } else {
+            ge_store(blkB + blockIdx.x, r);
+            ge_store(blkU + blockIdx.x, U);
+        }
+    }
+}
+__global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ blkB, const ge *__restrict__ blkU, uint32_t SB,
+                                                  int lgBL, uint32_t nmsm, uint32_t W, ge *__restrict__ rows_out) {
+    __shared__ ge sh[64];
+    const uint32_t row = blockIdx.x, t = threadIdx.x;
+    ge u, v;
+    if (t < SB) ge_load(u, blkU + (size_t)row * SB + t); else ge_identity(u);
+    ge_store(&sh[t], u);
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        __syncthreads();
+        ge a, b;
+        const bool act = t + d < 64;
+        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
+        __syncthreads();
+        if (act) ge_store(&sh[t], a);
+    }
+    __syncthreads();
+    if (t < SB) ge_load(v, blkB + (size_t)row * SB + t); else ge_identity(v);
+    if (t > 0 && t < SB) {
+        ge suf;
+        ge_load(suf, &sh[t]);
+        ge_dbl_n(suf, lgBL);   // B L suf_beta
+        ge_add(v, v, suf);
+    }
+    __syncthreads();
+    ge_store(&sh[t], v);
+    for (uint32_t w = 32; w >= 1; w >>= 1) {
+        __syncthreads();
+        if (t < w) {
+            ge a, b;
+            ge_load(a, &sh[t]); ge_load(b, &sh[t + w]);
+            ge_add(a, a, b);
+            ge_store(&sh[t], a);
+        }
+    }
+    if (t == 0) {
+        ge r; ge_load(r, &sh[0]);
+        ge_store(rows_out + row_perm(row, nmsm, W), r);
+    }
+}
+
 static int msm_window(uint64_t total) {
     int lg = 0;
     while ((1ULL << (lg + 1)) <= total) lg++;
@@ -1169,6 +1280,22 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         pout = a ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
     }
     hipLaunchKernelGGL(k_rbk_final, dim3(nblk(E, 64)), dim3(64), 0, st_, kin, pin, E, invalid, p.c, buckets, bflag);
+#if ROW_TWO_LEVEL
+    {
+        // P threads per row (power of two), L buckets each, blocks of B <= 256
+        const uint32_t P = std::min<uint32_t>((uint32_t)p.half, ROW_MAX_THREADS);
+        const uint32_t L = (uint32_t)p.half / P, B = std::min<uint32_t>(P, 256), SB = P / B;
+        int lgL = 0, lgBL = 0;
+        while ((1u << lgL) < L) lgL++;
+        while ((1u << lgBL) < B * L) lgBL++;
+        ge *blkB = AS_GE(segacc_.p), *blkU = blkB + (size_t)p.rows * SB;
+        hipLaunchKernelGGL(k_row_blocks, dim3(p.rows * SB), dim3(B), 0, st_, AS_CGE(buckets_.p), bflag,
+                           (uint32_t)p.half, L, lgL, SB, (uint32_t)nmsm, (uint32_t)p.W, blkB, blkU, AS_GE(rows_dev_.p));
+        if (SB > 1)
+            hipLaunchKernelGGL(k_row_final, dim3(p.rows), dim3(64), 0, st_, (const ge *)blkB, (const ge *)blkU, SB,
+                               lgBL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
+    }
+#else
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
     ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
     hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
@@ -1177,6 +1304,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     while ((1 << lgL) < p.seglen) lgL++;
     hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
                        (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
+#endif
     BPG_HIP(hipGetLastError());
     BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;

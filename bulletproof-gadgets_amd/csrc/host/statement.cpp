@@ -41,44 +41,46 @@ Var ConstraintSystem::commit_point(const uint8_t V[32]) {
     V_.insert(V_.end(), V, V + 32);
     return BPG_VAR(BPG_VAR_V, i);
 }
-// Prover::eval: sum coeff * value (dalek Mul/Add: canonical results)
+// Prover::eval: sum coeff * value (dalek Mul/Add: canonical results). The
+// statement layer's terms are mostly unit coefficients and constants (the
+// MiMC rounds' (One, c)): c * 1 = c mod l and 1 * v = v mod l, and Add
+// reduces its operands, so those terms are added without a multiplication;
+// a zero coefficient adds 0 to an already canonical sum.
+static inline bool sc_is_one(const Scalar &s) { return s.v[0] == 1 && !(s.v[1] | s.v[2] | s.v[3]); }
 Scalar ConstraintSystem::eval(const LC &lc) const {
     Scalar acc = Scalar::zero();
     for (auto &x : lc.t) {
-        uint32_t k = BPG_VAR_KIND(x.first), i = BPG_VAR_INDEX(x.first);
-        Scalar val;
-        switch (k) {
-            case BPG_VAR_ONE: val = Scalar::one(); break;
-            case BPG_VAR_L: val = aL_[i]; break;
-            case BPG_VAR_R: val = aR_[i]; break;
-            case BPG_VAR_O: val = aO_[i]; break;
-            default: val = v_[i]; break;
-        }
-        acc = acc + x.second * val;
+        const uint32_t k = BPG_VAR_KIND(x.first), i = BPG_VAR_INDEX(x.first);
+        if (x.second.is_zero_raw()) continue;
+        if (k == BPG_VAR_ONE) { acc = acc + x.second; continue; }
+        const Scalar &val = k == BPG_VAR_L ? aL_[i] : k == BPG_VAR_R ? aR_[i] : k == BPG_VAR_O ? aO_[i] : v_[i];
+        acc = acc + (sc_is_one(x.second) ? val : x.second * val);
     }
     return acc;
 }
 void ConstraintSystem::emit(const LC &lc) {
+    const size_t k0 = term_var_.size();
+    term_coeff_.resize(32 * (k0 + lc.t.size()));
+    uint8_t *c = term_coeff_.data() + 32 * k0;
     for (auto &x : lc.t) {
         term_var_.push_back(x.first);
-        uint8_t b[32];
-        x.second.to_bytes(b);
-        term_coeff_.insert(term_coeff_.end(), b, b + 32);
+        x.second.to_bytes(c);
+        c += 32;
     }
     row_ptr_.push_back((uint32_t)term_var_.size());
 }
 void ConstraintSystem::emit_minus(const LC &lc, Var v) {
     static const Scalar minus_one = -Scalar::one();
+    const size_t k0 = term_var_.size();
+    term_coeff_.resize(32 * (k0 + lc.t.size() + 1));
+    uint8_t *c = term_coeff_.data() + 32 * k0;
     for (auto &x : lc.t) {
         term_var_.push_back(x.first);
-        uint8_t b[32];
-        x.second.to_bytes(b);
-        term_coeff_.insert(term_coeff_.end(), b, b + 32);
+        x.second.to_bytes(c);
+        c += 32;
     }
     term_var_.push_back(v);
-    uint8_t b[32];
-    minus_one.to_bytes(b);
-    term_coeff_.insert(term_coeff_.end(), b, b + 32);
+    minus_one.to_bytes(c);
     row_ptr_.push_back((uint32_t)term_var_.size());
 }
 // r1cs Prover::multiply / Verifier::multiply: allocate (l, r, o), constrain
@@ -87,7 +89,7 @@ ConstraintSystem::Triple ConstraintSystem::multiply(const LC &left, const LC &ri
     uint32_t i = nvars_++;
     Triple t{BPG_VAR(BPG_VAR_L, i), BPG_VAR(BPG_VAR_R, i), BPG_VAR(BPG_VAR_O, i)};
     if (prover_) {
-        Scalar l = eval(left), r = eval(right);
+        Scalar l = eval(left), r = &left == &right ? l : eval(right);
         aL_.push_back(l); aR_.push_back(r); aO_.push_back(l * r);
     }
     if (stack_.empty()) {   // left - l = 0 and right - r = 0, without copying the combinations
@@ -232,16 +234,27 @@ Scalar mimc_sponge_native(const std::vector<Scalar> &blocks) {
 // mimc_hash_gadget.rs:108-150
 static LC mimc_sponge(ConstraintSystem &cs, const std::vector<LC> &pre) {
     const auto &consts = mimc_consts();
+    const Var one = var_one();
     LC key = LC::cnst(Scalar::zero());
     LC state = LC::cnst(Scalar::zero());
+    // the round's LCs are rebuilt in place (same terms, same order as
+    // p + key + LC::cnst(c), LC::of(sq.o), LC::of(sq.l)): no allocation per round
+    LC pk, so, sl;
+    so.t.resize(1);
+    sl.t.resize(1);
     for (const LC &v : pre) {
         state = state + v;
         LC p = state;
+        pk.t.reserve(p.t.size() + 2);
         for (const Scalar &c : consts) {
-            LC pk = p + key + LC::cnst(c);
+            pk.t.assign(p.t.begin(), p.t.end());
+            pk.t.push_back({one, Scalar::zero()});   // + key
+            pk.t.push_back({one, c});
             auto sq = cs.multiply(pk, pk);
-            auto cube = cs.multiply(LC::of(sq.o), LC::of(sq.l));
-            p = LC::of(cube.o);
+            so.t[0] = {sq.o, Scalar::one()};
+            sl.t[0] = {sq.l, Scalar::one()};
+            auto cube = cs.multiply(so, sl);
+            p.t.assign(1, {cube.o, Scalar::one()});
         }
         state = p + key;
     }
