@@ -473,7 +473,12 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
     // constraint matrix, transposed to columns [L | R | O | V | One]
     const uint32_t ncol = 3 * n + m + 1;
     P->ncol = ncol;
-    std::vector<uint32_t> cnt(ncol + 1, 0);
+    // transposition scratch, kept per thread across calls (c_prove prepares
+    // every statement: ~170 MB at 2^20, otherwise reallocated and page-faulted
+    // in each time)
+    static thread_local std::vector<uint32_t> cnt, pos, rows;
+    static thread_local std::vector<ScD> coef;
+    cnt.assign(ncol + 1, 0);
     const uint32_t nnz = cs->row_ptr[cs->q];
     auto colof = [&](uint32_t var) -> uint32_t {
         uint32_t kind = BPG_VAR_KIND(var), idx = BPG_VAR_INDEX(var);
@@ -488,8 +493,9 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
     };
     for (uint32_t k = 0; k < nnz; k++) cnt[colof(cs->term_var[k]) + 1]++;
     for (uint32_t c = 0; c < ncol; c++) cnt[c + 1] += cnt[c];
-    std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1), rows(nnz ? nnz : 1);
-    std::vector<ScD> coef(nnz ? nnz : 1);
+    pos.assign(cnt.begin(), cnt.end() - 1);
+    rows.resize(nnz ? nnz : 1);
+    coef.resize(nnz ? nnz : 1);
     for (uint32_t q = 0; q < cs->q; q++)
         for (uint32_t k = cs->row_ptr[q]; k < cs->row_ptr[q + 1]; k++) {
             uint32_t c = colof(cs->term_var[k]);

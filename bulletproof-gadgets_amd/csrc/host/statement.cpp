@@ -28,7 +28,39 @@ LC lc_scale(const LC &a, const Scalar &s) {
 }
 
 // -------------------------------------------------------- ConstraintSystem
-ConstraintSystem::ConstraintSystem(bool prover) : prover_(prover) {}
+// The flattened arrays of a 2^20 statement are ~200 MB; grown from empty for
+// every statement, their reallocation copies and first-touch page faults cost
+// about as much as the synthesis itself (and serialise threads on the
+// process's page tables). A thread keeps the buffers of its last recorder
+// (cleared, capacity intact) for the next one.
+namespace {
+struct CsBuffers {
+    std::vector<Scalar> aL, aR, aO;
+    std::vector<uint32_t> row_ptr, term_var;
+    std::vector<uint8_t> term_coeff, aLb, aRb, aOb;
+    bool valid = false;
+};
+CsBuffers &cs_pool() { static thread_local CsBuffers b; return b; }
+}  // namespace
+ConstraintSystem::ConstraintSystem(bool prover) : prover_(prover) {
+    CsBuffers &b = cs_pool();
+    if (b.valid) {
+        b.valid = false;
+        aL_.swap(b.aL); aR_.swap(b.aR); aO_.swap(b.aO);
+        row_ptr_.swap(b.row_ptr); term_var_.swap(b.term_var); term_coeff_.swap(b.term_coeff);
+        aLb_.swap(b.aLb); aRb_.swap(b.aRb); aOb_.swap(b.aOb);
+        aL_.clear(); aR_.clear(); aO_.clear(); term_var_.clear(); term_coeff_.clear();
+        row_ptr_.assign(1, 0);
+    }
+}
+ConstraintSystem::~ConstraintSystem() {
+    CsBuffers &b = cs_pool();
+    if (b.valid && b.term_coeff.capacity() >= term_coeff_.capacity()) return;   // keep the larger set
+    aL_.swap(b.aL); aR_.swap(b.aR); aO_.swap(b.aO);
+    row_ptr_.swap(b.row_ptr); term_var_.swap(b.term_var); term_coeff_.swap(b.term_coeff);
+    aLb_.swap(b.aLb); aRb_.swap(b.aRb); aOb_.swap(b.aOb);
+    b.valid = true;
+}
 
 Var ConstraintSystem::commit_value(const Scalar &v, const Scalar &blinding) {
     uint32_t i = (uint32_t)v_.size();

@@ -48,6 +48,7 @@ struct StatementError : std::runtime_error {
 class ConstraintSystem {
   public:
     explicit ConstraintSystem(bool prover);
+    ~ConstraintSystem();
     bool prover() const { return prover_; }
     Var commit_value(const Scalar &v, const Scalar &blinding);   // Prover::commit
     Var commit_point(const uint8_t V[32]);                        // Verifier::commit
