@@ -677,16 +677,28 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
             dist.barrier()
         torch.cuda.synchronize()
 
-    pool = ThreadPoolExecutor(threads)
-    list(pool.map(one, texts[:batch * a.warmup]))
-    barrier()
-    t0 = time.perf_counter()
-    outs = list(pool.map(one, texts[batch * a.warmup:]))
-    barrier()
-    dt = time.perf_counter() - t0
-    # the worker threads (and their per-thread device workspaces) end here,
-    # while the HIP runtime is certainly still up
-    pool.shutdown(wait=True)
+    if os.environ.get("BENCH_STATEMENTS_API") == "c_prove":   # one c_prove per statement per thread
+        pool = ThreadPoolExecutor(threads)
+        list(pool.map(one, texts[:batch * a.warmup]))
+        barrier()
+        t0 = time.perf_counter()
+        outs = list(pool.map(one, texts[batch * a.warmup:]))
+        barrier()
+        dt = time.perf_counter() - t0
+        # the worker threads (and their per-thread device workspaces) end
+        # here, while the HIP runtime is certainly still up
+        pool.shutdown(wait=True)
+        api = "c_prove on %d threads" % threads
+    else:   # bpg_prove_statements: lockstep RNG over distinct statements, device consumers
+        bpg.prove_statements("bench", texts[:batch * a.warmup], threads)
+        barrier()
+        t0 = time.perf_counter()
+        outs = bpg.prove_statements("bench", texts[batch * a.warmup:], threads)
+        barrier()
+        dt = time.perf_counter() - t0
+        if any(o is None for o in outs):
+            raise SystemExit("bench: a statement failed: %s" % bpg.last_error())
+        api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(16, max(1, threads // 2)))
     if dist is not None:
         dt = D.max_over_ranks(dt)
     last = texts[-1]
@@ -713,7 +725,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         "scaling": "weak", "vs_baseline": None, "dtype": "u32 (255-bit integer field/scalar arithmetic)",
         "data": "synthetic: %d distinct seeded config-5 statements per rank" % (batch * a.steps),
         "config": {"workload": W.NAMES[5], "q_constraints": q, "statements_per_step_per_gpu": batch,
-                   "host_threads_per_gpu": threads},
+                   "host_threads_per_gpu": threads, "api": api},
         "statements_per_s": round(n_st / dt, 2),
         "single_statement_ms": phases,
         "dist": DIST_INFO,

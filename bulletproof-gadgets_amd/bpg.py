@@ -31,7 +31,7 @@ EXPORTS = [
     "bpg_ctx_set_fold_pairs", "bpg_ctx_set_ipp_tail", "bpg_ctx_setup_stats", "bpg_r1cs_prove_sharded", "bpg_cs_create", "bpg_cs_free",
     "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
-    "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim",
+    "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim", "bpg_prove_statements",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -120,6 +120,7 @@ def lib():
         L.bpg_prepare_shard.argtypes = [vp, vp, u32, u32]
         L.bpg_prove_prepared.argtypes = [vp, vp, sz, vp, ALLGATHER_FN, vp, vp, sz, ctypes.POINTER(sz)]
         L.bpg_verify_prepared.argtypes = [vp, vp, sz, vp, vp, sz, vp, u32, u32, vp]
+        L.bpg_prove_statements.argtypes = [cp, vp, vp, vp, vp, u32, u32, vp]
         L.bpg_ctx_trim.restype = ctypes.c_int64
         L.bpg_ctx_trim.argtypes = [vp]
         L.bpg_cs_create.restype = vp
@@ -172,6 +173,32 @@ def prove(name, instance, witness, gadgets):
     finally:
         lib().free_proof(a)
     return proof, coms
+
+
+def prove_statements(name, statements, threads, seeds=None):
+    """bpg_prove_statements: prove.rs:37 for many distinct statements
+    ((instance, witness, gadgets) texts) at once; statement k behaves as
+    set_seed(seeds[k]); prove(name, *statements[k]). Returns a list of
+    (proof, coms) or None per statement."""
+    n = len(statements)
+    arr = lambda xs: (ctypes.c_char_p * max(n, 1))(*[_b(x) for x in xs])
+    ins, wit, gad = (arr([st[i] for st in statements]) for i in range(3))
+    sd = (ctypes.c_uint64 * max(n, 1))(*seeds) if seeds is not None else None
+    out = (ctypes.POINTER(ProofArtifacts) * max(n, 1))()
+    rc = lib().bpg_prove_statements(_b(name), ins, wit, gad, sd, n, threads, out)
+    if rc < 0:
+        raise BpgError(last_error())
+    res = []
+    for k in range(n):
+        a = out[k]
+        if not a:
+            res.append(None)
+            continue
+        try:
+            res.append((bytes(a.contents.proof[:a.contents.proof_len]), a.contents.commitments.decode()))
+        finally:
+            lib().free_proof(a)
+    return res
 
 
 def verify(name, instance, proof, commitments, gadgets):

@@ -481,6 +481,175 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
     }, -1);
 }
 
+// prove.rs:37-82 for `count` distinct statements (include/bpg.h): CPU
+// workers synthesise and upload statements and draw the TranscriptRng
+// streams of up to 8 of them in lockstep (rng_draw_multi); consumer threads
+// (one HIP stream each, mostly asleep on the device) run the device part.
+static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector<uint8_t> &proof) {
+    ProofArtifacts *a = (ProofArtifacts *)malloc(sizeof(ProofArtifacts));
+    char *c = (char *)malloc(coms.size() + 1);
+    uint8_t *p = (uint8_t *)malloc(proof.size() ? proof.size() : 1);
+    if (!a || !c || !p) { free(a); free(c); free(p); throw std::runtime_error("out of memory"); }
+    memcpy(c, coms.c_str(), coms.size() + 1);
+    memcpy(p, proof.data(), proof.size());
+    a->commitments = c;
+    a->proof = p;
+    a->proof_len = proof.size();
+    a->proof_cap = proof.size();
+    return a;
+}
+int bpg_prove_statements(const char *name, const char *const *instances, const char *const *witnesses,
+                         const char *const *gadgets, const uint64_t *seeds, uint32_t count, uint32_t threads,
+                         struct ProofArtifacts **out) {
+    return guarded([&]() -> int {
+        if (!name || (count && (!instances || !witnesses || !gadgets || !out))) throw std::runtime_error("NULL argument");
+        require_device();
+        if (!count) return 0;
+        for (uint32_t k = 0; k < count; k++) out[k] = nullptr;
+        const int device = g_device;
+        const uint32_t W = std::max<uint32_t>(1, threads);
+        const uint32_t C = std::min<uint32_t>(16, std::max<uint32_t>(1, W / 2));
+        const size_t label_len = strlen(name);
+        const uint8_t *label = (const uint8_t *)name;
+        struct Item {
+            uint32_t k;
+            std::unique_ptr<PreparedCS> cs;
+            std::string coms;
+            uint8_t entropy[32];
+            RngBlock rb;
+        };
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<std::unique_ptr<Item>> prepared, ready;
+        uint32_t next = 0, synth_busy = 0, rng_busy = 0, inflight = 0, done = 0, proved = 0;
+        const uint32_t limit = W + 8 + 2 * C;
+        std::string first_err;
+        bool fatal = false;
+        auto note_err = [&](uint32_t k, const std::string &e, bool hip) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (first_err.empty()) first_err = "statement " + std::to_string(k) + ": " + e;
+            if (hip) fatal = true;
+            cv.notify_all();
+        };
+        pool().run((int)(W + C), [&](int id) {
+            const bool worker = (uint32_t)id < W;
+            for (;;) {
+                std::vector<std::unique_ptr<Item>> group;
+                std::unique_ptr<Item> item;
+                uint32_t k = 0;
+                int what = 0;   // 1 synthesise k, 2 RNG group, 3 device
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] {
+                        if (fatal || done == count) return true;
+                        if (!worker) return !ready.empty();
+                        const bool tail = next == count && synth_busy == 0;
+                        if (prepared.size() >= 8 || (tail && !prepared.empty())) return true;
+                        return next < count && inflight < limit;
+                    });
+                    if (fatal || done == count) break;
+                    if (!worker) {
+                        item = std::move(ready.front());
+                        ready.pop_front();
+                        what = 3;
+                    } else if (prepared.size() >= 8 || (next == count && synth_busy == 0 && !prepared.empty())) {
+                        while (!prepared.empty() && group.size() < 8) {
+                            group.push_back(std::move(prepared.front()));
+                            prepared.pop_front();
+                        }
+                        rng_busy++;
+                        what = 2;
+                    } else {
+                        k = next++;
+                        synth_busy++;
+                        inflight++;
+                        what = 1;
+                    }
+                }
+                if (what == 1) {
+                    std::unique_ptr<Item> it(new Item());
+                    it->k = k;
+                    bool ok = false;
+                    try {
+                        EntropySource &e = thread_entropy();
+                        const EntropySource saved = e;
+                        if (seeds) { e.seeded = true; e.cs.seed(seeds[k]); }
+                        try {
+                            Synthesis syn = synthesize_prover(instances[k], witnesses[k], gadgets[k]);
+                            bpg_r1cs_view v = syn.cs->view(true);
+                            it->cs = prepare_cs(&v, device);
+                            for (size_t i = 0; i < syn.com_names.size(); i++)
+                                it->coms += syn.com_names[i] + " = 0x" + hex32(it->cs->V.data() + 32 * i) + "\n";
+                            e.fill(it->entropy, 32);
+                        } catch (...) {
+                            e = saved;
+                            throw;
+                        }
+                        e = saved;
+                        it->rb.wide = it->cs->slots(1, 2 * (size_t)it->cs->n * 64 + 64)[0];
+                        it->rb.on_device = true;
+                        ok = true;
+                    } catch (const dev::HipError &e) {
+                        note_err(k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr, true);
+                    } catch (const std::exception &e) {
+                        note_err(k, e.what(), false);
+                    }
+                    std::lock_guard<std::mutex> lk(mu);
+                    synth_busy--;
+                    if (ok) prepared.push_back(std::move(it));
+                    else { inflight--; done++; }
+                    cv.notify_all();
+                } else if (what == 2) {
+                    try {
+                        const PreparedCS *cs[8];
+                        const uint8_t *ent[8];
+                        RngBlock *rb[8];
+                        for (size_t i = 0; i < group.size(); i++) {
+                            cs[i] = group[i]->cs.get();
+                            ent[i] = group[i]->entropy;
+                            rb[i] = &group[i]->rb;
+                        }
+                        rng_draw_multi(cs, label, label_len, ent, (int)group.size(), rb);
+                    } catch (const dev::HipError &e) {
+                        note_err(group[0]->k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr,
+                                 true);
+                    } catch (const std::exception &e) {
+                        note_err(group[0]->k, e.what(), true);
+                    }
+                    std::lock_guard<std::mutex> lk(mu);
+                    rng_busy--;
+                    for (auto &g : group) ready.push_back(std::move(g));
+                    cv.notify_all();
+                } else {
+                    try {
+                        std::vector<uint8_t> pr = gpu_prove_rng(*item->cs, label, label_len, item->rb);
+                        out[item->k] = make_artifacts(item->coms, pr);
+                        std::lock_guard<std::mutex> lk(mu);
+                        proved++;
+                    } catch (const dev::HipError &e) {
+                        note_err(item->k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr, true);
+                    } catch (const std::exception &e) {
+                        note_err(item->k, e.what(), false);
+                    }
+                    item.reset();   // frees the statement's device arrays
+                    std::lock_guard<std::mutex> lk(mu);
+                    inflight--;
+                    done++;
+                    cv.notify_all();
+                }
+            }
+        });
+        if (fatal) {
+            for (uint32_t k = 0; k < count; k++) { free_proof(out[k]); out[k] = nullptr; }
+            throw std::runtime_error(first_err);
+        }
+        if (!first_err.empty()) set_err(first_err);
+        const int n_ok = (int)proved;
+        if (n_ok < (int)count) g_err = first_err;   // guarded() cleared it on entry; keep the reason
+        return n_ok;
+    }, -1);
+}
+
 // Verifier::verify (verify.rs:71) over `count` proofs of one prepared
 // circuit: each worker thread verifies whole proofs on its own HIP stream
 // (proofs are independent; the sharded single-proof path is

@@ -648,12 +648,11 @@ static Transcript prover_transcript(const PreparedCS &cs, const uint8_t *label, 
 // forked from the transcript before any challenge, so all draws can be made
 // before the device work starts. Up to 8 proofs run in lockstep (Strobe8).
 // The producers' host-to-device copies (95 MB per 2^20 proof, a few GB/s in
-// all) go to BPG_PRODUCER_STREAMS streams per device shared by all producer
-// threads (default 1; 0: one stream per producer thread). Every HIP stream
-// takes one of the process's GPU_MAX_HW_QUEUES hardware queues, and streams
-// beyond that share queues in order, so a consumer stream that shared a
-// queue with a producer waited behind its copies (and the copies behind its
-// kernels).
+// all) go to one stream per producer thread (default), or with
+// BPG_PRODUCER_STREAMS=k to k streams shared by all producer threads. One
+// shared stream (fewer streams than hardware queues for the consumers)
+// measured 62.3 / 62.4 vs 70.8 / 69.7 M constraints/s with a stream per
+// producer (profiles/r03a_ab_producer_streams.txt).
 static hipStream_t shared_producer_stream(int device, int nstreams) {
     static std::mutex mu;
     static std::map<int, std::vector<hipStream_t>> streams;
@@ -670,7 +669,7 @@ static hipStream_t shared_producer_stream(int device, int nstreams) {
 }
 ProducerStage &producer_stage(int device) {
     static thread_local std::map<int, std::unique_ptr<ProducerStage>> m;
-    static const int nshared = [] { const char *e = getenv("BPG_PRODUCER_STREAMS"); return e ? atoi(e) : 1; }();
+    static const int nshared = [] { const char *e = getenv("BPG_PRODUCER_STREAMS"); return e ? atoi(e) : 0; }();
     auto &p = m[device];
     if (!p) {
         BPG_HIP(hipSetDevice(device));
@@ -753,6 +752,69 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         S.draw64(tp);
         for (int k = 0; k < count; k++) out[k]->tb[j] = Scalar::from_wide(tmp[k]);
     }
+}
+
+// The same for proofs of up to 8 DIFFERENT statements (bpg_prove_statements):
+// each statement's TranscriptRng runs on its own until its first draw
+// (i_bl), which leaves every STROBE state at byte 64 after a permutation, so
+// the remaining draws run in lockstep although the transcripts differ. Lane
+// k draws o_bl, s_bl, 2 n_k wide scalars (to out[k]->wide, a device buffer)
+// and the five t blindings; lanes with fewer gates write their surplus
+// draws to scratch.
+void rng_draw_multi(const PreparedCS *const *cs, const uint8_t *label, size_t label_len,
+                    const uint8_t *const *entropy, int count, RngBlock *const *out) {
+    if (count < 1 || count > 8) throw std::runtime_error("rng group size");
+    std::vector<TranscriptRng> rng;
+    rng.reserve(count);
+    uint8_t first[64];
+    const Strobe128 *st[8];
+    uint64_t D[8], maxD = 0;   // draws after i_bl: o_bl, s_bl, 2n wide, 5 t blindings
+    for (int k = 0; k < count; k++) {
+        Transcript T = prover_transcript(*cs[k], label, label_len);
+        rng.emplace_back(T);
+        for (uint32_t i = 0; i < cs[k]->m; i++)
+            rng.back().rekey_with_witness_bytes("v_blinding", (const uint8_t *)cs[k]->vb[i].v, 32);
+        rng.back().finalize(entropy[k]);
+        rng.back().fill_bytes(first, 64);
+        out[k]->i_bl = Scalar::from_wide(first);
+        D[k] = 2 + 2 * (uint64_t)cs[k]->n + 5;
+        maxD = std::max(maxD, D[k]);
+    }
+    for (int k = 0; k < count; k++) st[k] = &rng[k].s;
+    Strobe8 S;
+    if (!S.from_each(st, count)) throw std::runtime_error("rng lockstep: states out of step");
+    uint8_t tmp[8][64], junk[64];
+    uint8_t *wp[8];
+    ProducerStage &ps = producer_stage(cs[0]->device);
+    const uint32_t CH = ProducerStage::CHUNK;
+    int buf = 0;
+    for (uint64_t d0 = 0; d0 < maxD; d0 += CH, buf ^= 1) {
+        const uint32_t len = (uint32_t)std::min<uint64_t>(CH, maxD - d0);
+        event_wait(ps.ev[buf]);
+        uint8_t *stg = ps.host[buf];   // lane k's draws d0 .. d0 + len at stg + k CH 64
+        for (uint32_t i = 0; i < len; i++) {
+            for (int k = 0; k < 8; k++) wp[k] = k < count ? stg + ((size_t)k * CH + i) * 64 : junk;
+            S.draw64(wp);
+        }
+        for (int k = 0; k < count; k++) {
+            const uint8_t *lane = stg + (size_t)k * CH * 64;
+            const uint64_t w0 = 2, w1 = 2 + 2 * (uint64_t)cs[k]->n;   // the wide draws [w0, w1)
+            for (uint64_t d = d0; d < d0 + len && d < D[k]; d++) {
+                const uint8_t *x = lane + (d - d0) * 64;
+                if (d == 0) out[k]->o_bl = Scalar::from_wide(x);
+                else if (d == 1) out[k]->s_bl = Scalar::from_wide(x);
+                else if (d >= w1) out[k]->tb[d - w1] = Scalar::from_wide(x);
+            }
+            const uint64_t a = std::max(d0, w0), b = std::min<uint64_t>(d0 + len, w1);
+            if (a < b)
+                BPG_HIP(hipMemcpyAsync(out[k]->wide + 64 * (a - w0), lane + (a - d0) * 64, (size_t)(b - a) * 64,
+                                       hipMemcpyHostToDevice, ps.st));
+        }
+        BPG_HIP(hipEventRecord(ps.ev[buf], ps.st));
+    }
+    event_wait(ps.ev[0]);
+    event_wait(ps.ev[1]);
+    (void)tmp;
 }
 
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,

@@ -143,6 +143,10 @@ ProducerStage &producer_stage(int device);
 // dev_out the s_L | s_R draws go to out[k]->wide as device buffers.
 void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
                     int count, RngBlock *const *out, bool dev_out);
+// The same for up to 8 proofs of DIFFERENT prepared statements (lockstep
+// after each statement's first draw); wide draws go to device buffers.
+void rng_draw_multi(const PreparedCS *const *cs, const uint8_t *label, size_t label_len,
+                    const uint8_t *const *entropy, int count, RngBlock *const *out);
 // Collective of the sharded prover: every rank contributes `bytes` and
 // receives world x bytes in rank order (an all-gather; the caller supplies
 // it, e.g. torch.distributed over RCCL).

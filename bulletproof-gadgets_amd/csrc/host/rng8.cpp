@@ -87,6 +87,20 @@ void Strobe8::from(const Strobe128 &s, int n) {
         for (int k = 0; k < 8; k++) L[i][k] = w[i];
     pos = s.pos; pos_begin = s.pos_begin; cur_flags = s.cur_flags;
 }
+bool Strobe8::from_each(const Strobe128 *const *s, int n) {
+    if (n < 1 || n > 8) return false;
+    for (int k = 1; k < n; k++)
+        if (s[k]->pos != s[0]->pos || s[k]->pos_begin != s[0]->pos_begin || s[k]->cur_flags != s[0]->cur_flags)
+            return false;
+    nstates = n;
+    for (int k = 0; k < 8; k++) {
+        uint64_t w[25];
+        memcpy(w, s[k < n ? k : 0]->st, 200);
+        for (int i = 0; i < 25; i++) L[i][k] = w[i];
+    }
+    pos = s[0]->pos; pos_begin = s[0]->pos_begin; cur_flags = s[0]->cur_flags;
+    return true;
+}
 void Strobe8::run_f() {
     for (int s = 0; s < 8; s++) { byte(s, pos) ^= pos_begin; byte(s, pos + 1) ^= 0x04; byte(s, S8_R + 1) ^= 0x80; }
     if (nstates == 1) {   // single proof (latency path): the scalar permutation is faster

@@ -22,6 +22,10 @@ struct Strobe8 {
     uint8_t pos, pos_begin, cur_flags;
     int nstates;
     void from(const Strobe128 &s, int n);              // n copies of one state
+    // n distinct states (proofs of different statements) that sit at the same
+    // byte position and operation (true after any draw: its prf permutes
+    // first, so every state ends at pos 64); false if they do not
+    bool from_each(const Strobe128 *const *s, int n);
     void meta_ad(const uint8_t *d, size_t len);        // same data for every state
     void key_each(const uint8_t *const *d, size_t len);  // per-state key material
     // TranscriptRng::fill_bytes(64) on every state; out[s] receives 64 bytes

@@ -64,6 +64,22 @@ void free_proof(struct ProofArtifacts *artifacts);
 /* Added: thread-local description of the last error ("" if none). */
 const char *bpg_last_error(void);
 
+/* Added: prove.rs:37-82 for `count` DISTINCT statements at once (a serving
+ * prover's batch). Statement k is parsed, synthesised and proved exactly as
+ * c_prove(name, instances[k], witnesses[k], gadgets[k]) on a thread whose
+ * thread_rng stream is seeded with seeds[k] (bpg_set_seed semantics;
+ * seeds == NULL: OS entropy), and out[k] receives what that c_prove returns
+ * (release with free_proof), or NULL if statement k failed. `threads` CPU
+ * workers synthesise and upload statements and draw the TranscriptRng
+ * streams of up to 8 statements in lockstep; min(16, threads / 2) more
+ * threads drive the device, one HIP stream each. Returns the number of
+ * statements proved (bpg_last_error() names the first failure), < 0 on a
+ * device error (then every out[k] is NULL). */
+int bpg_prove_statements(const char *name, const char *const *instances,
+                         const char *const *witnesses, const char *const *gadgets,
+                         const uint64_t *seeds, uint32_t count, uint32_t threads,
+                         struct ProofArtifacts **out);
+
 /* Added: `prover.num_constraints()` of the last c_prove on this thread
  * (the reference prints it from prove.rs:75; the CLI prints it here). */
 uint64_t bpg_last_num_constraints(void);
