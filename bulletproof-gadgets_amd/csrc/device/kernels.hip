@@ -926,8 +926,12 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
     }
 }
 
-// Window rows in two launches spread over many blocks (ROW_TWO_LEVEL, the
-// default; else k_bucket_seg + k_row_reduce above, one block per row).
+// Window rows in two launches spread over many blocks (ROW_TWO_LEVEL=1;
+// default k_bucket_seg + k_row_reduce above, one block per row). The
+// two-level form cuts a 2^15-bucket row's latency from ~270 to ~85 us of
+// serial point additions but adds ~35% more additions (the block scans),
+// and with the chip full of other streams' work the added VALU work costs
+// more than the latency it hides.
 // Row r is cut into SB blocks of B threads, thread t of block beta owning the
 // L buckets [s L, s L + L) of segment s = beta B + t:
 //   A_s = sum_j (j+1) S_{sL+j},  T_s = sum_j S_{sL+j}   (running sum, 2L adds)
@@ -938,7 +942,7 @@ __global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA,
 // sum_{t>=1} suf_t). k_row_blocks writes (Bb, U) per block; k_row_final does
 // the same weighted combine over the SB blocks of a row (one wave per row).
 #ifndef ROW_TWO_LEVEL
-#define ROW_TWO_LEVEL 1
+#define ROW_TWO_LEVEL 0   // measured slower: 69.3 / 69.4 vs 71.8 / 71.8 M (profiles/r03b_ab_row_two_level.txt)
 #endif
 #define ROW_MAX_THREADS 4096   // threads per row (segments of L = half / 4096 buckets at c = 16)
 __global__ __launch_bounds__(256) void k_row_blocks(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
@@ -2046,8 +2050,14 @@ DEVI void foldn_get(gec &c, const uint32_t *tb) {
 #pragma unroll
     for (int k = 0; k < 40; k++) w[k] = tb[k * 64];
 }
+#ifndef FOLD3_WAVES
+#define FOLD3_WAVES 1      // waves per SIMD the triple fold is compiled for
+#endif
+#ifndef FOLD3_PREFETCH
+#define FOLD3_PREFETCH 1   // the next op's table entry is loaded before the doublings
+#endif
 template <class P>
-__global__ __launch_bounds__(64, 1) void k_ipp_fold3(const FoldNArgs *__restrict__ Ap) {
+__global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *__restrict__ Ap) {
     const FoldNArgs &A = *Ap;
     uint32_t b = blockIdx.x, sg = 0;
     for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
@@ -2096,6 +2106,7 @@ __global__ __launch_bounds__(64, 1) void k_ipp_fold3(const FoldNArgs *__restrict
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
+#if FOLD3_PREFETCH
     gec c;
     if (nops > 1) foldn_get(c, entry(fold2_op(ops, 1)));
     for (uint32_t k = 1; k < nops; k++) {
@@ -2110,6 +2121,21 @@ __global__ __launch_bounds__(64, 1) void k_ipp_fold3(const FoldNArgs *__restrict
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
         c = cn;
     }
+#else
+    // no entry held across the doublings (40 fewer VGPRs): the entry's load
+    // latency is left to the other waves of the SIMD
+    for (uint32_t k = 1; k < nops; k++) {
+        const uint32_t op = fold2_op(ops, k);
+        const uint32_t g = op & 255;
+        if (g) {
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        gec c;
+        foldn_get(c, entry(op));
+        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+    }
+#endif
     const uint32_t tail = A.tail[sg];
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);

@@ -884,15 +884,18 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     Transcript T = prover_transcript(cs, label, label_len);
     const Scalar i_bl = rb.i_bl, o_bl = rb.o_bl, s_bl = rb.s_bl;
 
-    // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G> (blinding terms added on the host)
+    // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G>, S1 = <s_L,G> + <s_R,H>
+    // (blinding terms added on the host): one MSM job of three MSMs, or
+    // (COMMIT_ONE_JOB=0) A_I1/A_O1 and S1 as two jobs
     PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
     MsmPlan pA{}, pS{};
     const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
     const int64_t gneg = gs->N;             // their negations follow each vector
-    if (nl) {
-        MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg},
-                          {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg},
-                          {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg}};
+    static const bool one_job = [] { const char *e = getenv("BPG_COMMIT_ONE_JOB"); return !e || e[0] != '0'; }();
+    const MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg},
+                            {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg},
+                            {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg}};
+    if (nl && !one_job) {
         int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
         pA = ws.msm->enqueue(segA, 3, 2, rowsA, MSM_NIELS);
         ws.prof_end(ph);
@@ -910,17 +913,26 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         }
         launch_wide_reduce(wd, nl, world, rank, as<ScD>(ws.sL), st);
         launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(ws.sR), st);
-        MsmSeg segS[2] = {{as<ScD>(ws.sL), G0, nl, 0, gneg}, {as<ScD>(ws.sR), H0, nl, 0, gneg}};
-        int ph = ws.prof_begin("msm_commit", 2.0 * nl * (64 + 32));
-        pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
-        ws.prof_end(ph);
+        if (one_job) {
+            const MsmSeg seg[5] = {segA[0], segA[1], segA[2], {as<ScD>(ws.sL), G0, nl, 2, gneg},
+                                   {as<ScD>(ws.sR), H0, nl, 2, gneg}};
+            int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
+            pA = ws.msm->enqueue(seg, 5, 3, rowsA, MSM_NIELS);
+            ws.prof_end(ph);
+        } else {
+            MsmSeg segS[2] = {{as<ScD>(ws.sL), G0, nl, 0, gneg}, {as<ScD>(ws.sR), H0, nl, 0, gneg}};
+            int ph = ws.prof_begin("msm_commit", 2.0 * nl * (64 + 32));
+            pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
+            ws.prof_end(ph);
+        }
     }
     ws.sync();
     Point AIS[3], tmp;
     if (nl) {
         combine_rows(AIS[0], rowsA, pA.W, pA.c);
         combine_rows(AIS[1], rowsA + pA.W, pA.W, pA.c);
-        combine_rows(AIS[2], rowsS, pS.W, pS.c);
+        if (one_job) combine_rows(AIS[2], rowsA + 2 * pA.W, pA.W, pA.c);
+        else combine_rows(AIS[2], rowsS, pS.W, pS.c);
     } else {
         pt_identity(AIS[0]); pt_identity(AIS[1]); pt_identity(AIS[2]);
     }
