@@ -1041,6 +1041,142 @@ __global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ blkB, c
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small MSMs (the IPP tail rounds, small circuits): no global sort and no
+// run-merge passes. One launch writes every point's signed radix-2^9 digits,
+// a second runs one block per window row: the row's points are counted-
+// sorted by bucket in LDS a tile at a time, thread t keeps bucket t's sum in
+// registers over all tiles (the next point of its list in flight while it
+// adds the current one), and the block ends with R = sum_t (t+1) S_t as a
+// suffix scan plus a tree sum in LDS. Two launches per job instead of ~14;
+// the IPP tail runs 12 such jobs per 2^20 proof.
+// ---------------------------------------------------------------------------
+#define SMSM_C 9
+#define SMSM_HALF 256                 // buckets per row = threads per block
+#define SMSM_W ((254 + SMSM_C - 1) / SMSM_C)
+#define SMSM_TILE 2048
+#ifndef SMSM_MAX
+#define SMSM_MAX 0                    // jobs of at most this many points (0: off; env BPG_SMALL_MSM)
+#endif
+__global__ void k_smsm_digits(SegTab T, uint32_t total, int16_t *__restrict__ dig) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    const int si = seg_of(T, g);
+    sc k;
+    sc_load(k, T.scal[si] + (g - T.gofs[si]));
+    const uint32_t mask = (1u << SMSM_C) - 1, full = 1u << SMSM_C;
+    uint32_t carry = 0;
+    for (int w = 0; w < SMSM_W; w++) {
+        const int bit = w * SMSM_C, lo = bit >> 5, sh = bit & 31;
+        uint64_t x = k.v[lo];
+        if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
+        const uint32_t d = ((uint32_t)(x >> sh) & mask) + carry;
+        int v;
+        if (d > SMSM_HALF) { v = -(int)(full - d); carry = 1; }
+        else { v = (int)d; carry = 0; }
+        dig[(size_t)w * total + g] = (int16_t)v;
+    }
+}
+struct SmsmRows { uint32_t moff[4], mtot[4]; };
+template <int FMT, bool NEGC>
+__global__ __launch_bounds__(SMSM_HALF) void k_smsm_rows(SegTab T, const int16_t *__restrict__ dig, uint32_t total,
+                                                         uint32_t nmsm, SmsmRows R, ge *__restrict__ rows_out) {
+    typedef typename BaseOf<FMT>::T BT;
+    __shared__ uint32_t cnt[SMSM_HALF], off[SMSM_HALF];
+    __shared__ uint32_t list[SMSM_TILE];
+    __shared__ uint64_t sptr[2 * MSM_MAXSEG];
+    __shared__ ge sh[SMSM_HALF];
+    const uint32_t t = threadIdx.x, row = blockIdx.x;
+    const uint32_t w = row / nmsm, m = row % nmsm;
+    const uint32_t g0 = R.moff[m], n = R.mtot[m];
+    if (t < MSM_MAXSEG) {
+        sptr[t] = reinterpret_cast<uint64_t>(T.base[t]);
+        sptr[MSM_MAXSEG + t] = reinterpret_cast<uint64_t>(T.neg[t]);
+    }
+    ge acc;
+    ge_identity(acc);
+    bool real = false;
+    constexpr int PER = SMSM_TILE / SMSM_HALF;
+    for (uint32_t t0 = 0; t0 < n; t0 += SMSM_TILE) {
+        cnt[t] = 0;
+        __syncthreads();
+        int16_t dd[PER];
+        uint32_t loc[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const uint32_t i = t0 + j * SMSM_HALF + t;
+            dd[j] = 0;
+            if (i < n) {
+                const uint32_t g = g0 + i;
+                dd[j] = dig[(size_t)w * total + g];
+                const int si = seg_of(T, g);
+                loc[j] = (uint32_t)si << MSM_SEG_SHIFT | (g - T.gofs[si]);
+                if (dd[j]) atomicAdd(&cnt[(dd[j] < 0 ? -dd[j] : dd[j]) - 1], 1u);
+            }
+        }
+        __syncthreads();
+        // exclusive starts of the buckets (Hillis-Steele over 256 counters)
+        const uint32_t mine = cnt[t];
+        off[t] = mine;
+        for (uint32_t d = 1; d < SMSM_HALF; d <<= 1) {
+            __syncthreads();
+            const uint32_t a = t >= d ? off[t - d] : 0u;
+            __syncthreads();
+            off[t] += a;
+        }
+        __syncthreads();
+        const uint32_t start = off[t] - mine;
+        __syncthreads();
+        off[t] = start;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            if (dd[j]) {
+                const uint32_t b = (dd[j] < 0 ? -dd[j] : dd[j]) - 1;
+                list[atomicAdd(&off[b], 1u)] = loc[j] | (dd[j] < 0 ? 0x80000000u : 0u);
+            }
+        }
+        __syncthreads();
+        // bucket t: its points of this tile, the next one in flight
+        if (mine) {
+            BT p;
+            uint32_t v = list[start];
+            msm_load_base<FMT, NEGC>(p, sptr, v);
+            for (uint32_t k = 0; k < mine; k++) {
+                BT use = p;
+                const uint32_t cur = v;
+                if (k + 1 < mine) { v = list[start + k + 1]; msm_load_base<FMT, NEGC>(p, sptr, v); }
+                if (real) msm_add_loaded<NEGC>(acc, use, cur >> 31);
+                else { msm_init_loaded<NEGC>(acc, use, cur >> 31); real = true; }
+            }
+        }
+        __syncthreads();
+    }
+    // R = sum_t (t+1) S_t = sum_t suf_t, suf_t = sum_{u >= t} S_u
+    ge_store(&sh[t], acc);
+    for (uint32_t d = 1; d < SMSM_HALF; d <<= 1) {
+        __syncthreads();
+        ge a, b;
+        const bool act = t + d < SMSM_HALF;
+        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
+        __syncthreads();
+        if (act) ge_store(&sh[t], a);
+    }
+    for (uint32_t h = SMSM_HALF / 2; h >= 1; h >>= 1) {
+        __syncthreads();
+        if (t < h) {
+            ge a, b;
+            ge_load(a, &sh[t]); ge_load(b, &sh[t + h]);
+            ge_add(a, a, b);
+            ge_store(&sh[t], a);
+        }
+    }
+    if (t == 0) {
+        ge r; ge_load(r, &sh[0]);
+        ge_store(rows_out + row_perm(row, nmsm, SMSM_W), r);
+    }
+}
+
 static int msm_window(uint64_t total) {
     int lg = 0;
     while ((1ULL << (lg + 1)) <= total) lg++;
@@ -1186,6 +1322,38 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
                                   : segs[i].base;
         negc = negc && segs[i].negofs != 0;
         T.row0[i] = segs[i].msm;
+    }
+    static const uint32_t smsm_max = [] {
+        const char *e = getenv("BPG_SMALL_MSM");
+        return e ? (uint32_t)atol(e) : (uint32_t)SMSM_MAX;
+    }();
+    if (total > 0 && total <= smsm_max && nmsm <= 4) {   // small job: two launches (k_smsm_*)
+        p.c = SMSM_C;
+        p.W = SMSM_W;
+        p.rows = nmsm * p.W;
+        p.half = SMSM_HALF;
+        p.E0 = (uint64_t)p.W * total;
+        p.passes = 0;
+        keys_.grow((size_t)p.W * total * sizeof(int16_t) + 256);
+        rows_dev_.grow((size_t)p.rows * sizeof(ge));
+        int16_t *dig = reinterpret_cast<int16_t *>(keys_.p);
+        SmsmRows R{};
+        for (int m = 0; m < nmsm; m++) { R.moff[m] = moff[m]; R.mtot[m] = mtot[m]; }
+        ProfScope ps(fmt == MSM_CACHED ? "msm_small_cached" : "msm_small_niels", 96.0 * (double)total,
+                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);
+        hipLaunchKernelGGL(k_smsm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, dig);
+        if (fmt == MSM_NIELS && negc)
+            hipLaunchKernelGGL((k_smsm_rows<MSM_NIELS, true>), dim3(p.rows), dim3(SMSM_HALF), 0, st_, T, dig,
+                               (uint32_t)total, (uint32_t)nmsm, R, AS_GE(rows_dev_.p));
+        else if (fmt == MSM_NIELS)
+            hipLaunchKernelGGL((k_smsm_rows<MSM_NIELS, false>), dim3(p.rows), dim3(SMSM_HALF), 0, st_, T, dig,
+                               (uint32_t)total, (uint32_t)nmsm, R, AS_GE(rows_dev_.p));
+        else
+            hipLaunchKernelGGL((k_smsm_rows<MSM_CACHED, false>), dim3(p.rows), dim3(SMSM_HALF), 0, st_, T, dig,
+                               (uint32_t)total, (uint32_t)nmsm, R, AS_GE(rows_dev_.p));
+        BPG_HIP(hipGetLastError());
+        BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
+        return p;
     }
     p.E0 = (uint64_t)p.W * total;
     p.T = RBK_T;
