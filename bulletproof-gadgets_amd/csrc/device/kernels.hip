@@ -228,9 +228,43 @@ DEVI int seg_of(const SegTab &T, uint32_t g) {
 // w * nmsm + msm), so
 // with the entries laid out [w][g] and segments ordered by MSM, the key array
 // is already grouped by row: the sort only orders each row by slot.
+// The same launch also clears the job's bucket flags and writes the sort's
+// tile table (5 words per tile: start, end, first tile of the row, one past
+// its last, row start; then each row's first tile), computed from the job's
+// geometry instead of being built on the host and copied up per job.
+struct TileGeo {
+    uint32_t nt, rows, tile, TW;      // tiles, rows, entries per tile, tiles per window
+    uint32_t moff[4], mtot[4], tpr[4], cum[4];
+    uint8_t *bflag;                   // cleared: bflag_bytes (multiple of 16)
+    uint64_t bflag_bytes;
+    uint32_t *tiles;                  // null: the host wrote the table
+};
 __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
-                             uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                             uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G) {
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint64_t q = g; q < G.bflag_bytes / 16; q += stride) reinterpret_cast<uint4 *>(G.bflag)[q] = uint4{0, 0, 0, 0};
+    if (G.tiles) {
+        for (uint32_t x = g; x < G.nt + G.rows; x += stride) {
+            if (x < G.nt) {
+                const uint32_t w = x / G.TW, rem = x % G.TW;
+                uint32_t m = 0;
+                while (m + 1 < nmsm && rem >= G.cum[m + 1]) m++;
+                const uint32_t j = rem - G.cum[m];
+                const uint32_t rs = w * total + G.moff[m];
+                const uint32_t first = w * G.TW + G.cum[m];
+                uint32_t *e = G.tiles + 5 * (size_t)x;
+                e[0] = rs + j * G.tile;
+                e[1] = rs + min(G.mtot[m], (j + 1) * G.tile);
+                e[2] = first;
+                e[3] = first + G.tpr[m];
+                e[4] = rs;
+            } else {
+                const uint32_t r = x - G.nt;
+                G.tiles[5 * (size_t)G.nt + r] = (r / nmsm) * G.TW + G.cum[r % nmsm];
+            }
+        }
+    }
     if (g >= total) return;
     int si = seg_of(T, g);
     sc k;
@@ -1041,149 +1075,28 @@ __global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ blkB, c
     }
 }
 
-// ---------------------------------------------------------------------------
-// Small MSMs (the IPP tail rounds, small circuits): no global sort and no
-// run-merge passes. One launch writes every point's signed radix-2^9 digits,
-// a second runs one block per window row: the row's points are counted-
-// sorted by bucket in LDS a tile at a time, thread t keeps bucket t's sum in
-// registers over all tiles (the next point of its list in flight while it
-// adds the current one), and the block ends with R = sum_t (t+1) S_t as a
-// suffix scan plus a tree sum in LDS. Two launches per job instead of ~14;
-// the IPP tail runs 12 such jobs per 2^20 proof.
-// ---------------------------------------------------------------------------
-#define SMSM_C 9
-#define SMSM_HALF 256                 // buckets per row = threads per block
-#define SMSM_W ((254 + SMSM_C - 1) / SMSM_C)
-#define SMSM_TILE 2048
-#ifndef SMSM_MAX
-#define SMSM_MAX 0                    // jobs of at most this many points (0: off; env BPG_SMALL_MSM)
-#endif
-__global__ void k_smsm_digits(SegTab T, uint32_t total, int16_t *__restrict__ dig) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    const int si = seg_of(T, g);
-    sc k;
-    sc_load(k, T.scal[si] + (g - T.gofs[si]));
-    const uint32_t mask = (1u << SMSM_C) - 1, full = 1u << SMSM_C;
-    uint32_t carry = 0;
-    for (int w = 0; w < SMSM_W; w++) {
-        const int bit = w * SMSM_C, lo = bit >> 5, sh = bit & 31;
-        uint64_t x = k.v[lo];
-        if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
-        const uint32_t d = ((uint32_t)(x >> sh) & mask) + carry;
-        int v;
-        if (d > SMSM_HALF) { v = -(int)(full - d); carry = 1; }
-        else { v = (int)d; carry = 0; }
-        dig[(size_t)w * total + g] = (int16_t)v;
-    }
-}
-struct SmsmRows { uint32_t moff[4], mtot[4]; };
-template <int FMT, bool NEGC>
-__global__ __launch_bounds__(SMSM_HALF) void k_smsm_rows(SegTab T, const int16_t *__restrict__ dig, uint32_t total,
-                                                         uint32_t nmsm, SmsmRows R, ge *__restrict__ rows_out) {
-    typedef typename BaseOf<FMT>::T BT;
-    __shared__ uint32_t cnt[SMSM_HALF], off[SMSM_HALF];
-    __shared__ uint32_t list[SMSM_TILE];
-    __shared__ uint64_t sptr[2 * MSM_MAXSEG];
-    __shared__ ge sh[SMSM_HALF];
-    const uint32_t t = threadIdx.x, row = blockIdx.x;
-    const uint32_t w = row / nmsm, m = row % nmsm;
-    const uint32_t g0 = R.moff[m], n = R.mtot[m];
-    if (t < MSM_MAXSEG) {
-        sptr[t] = reinterpret_cast<uint64_t>(T.base[t]);
-        sptr[MSM_MAXSEG + t] = reinterpret_cast<uint64_t>(T.neg[t]);
-    }
-    ge acc;
-    ge_identity(acc);
-    bool real = false;
-    constexpr int PER = SMSM_TILE / SMSM_HALF;
-    for (uint32_t t0 = 0; t0 < n; t0 += SMSM_TILE) {
-        cnt[t] = 0;
-        __syncthreads();
-        int16_t dd[PER];
-        uint32_t loc[PER];
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            const uint32_t i = t0 + j * SMSM_HALF + t;
-            dd[j] = 0;
-            if (i < n) {
-                const uint32_t g = g0 + i;
-                dd[j] = dig[(size_t)w * total + g];
-                const int si = seg_of(T, g);
-                loc[j] = (uint32_t)si << MSM_SEG_SHIFT | (g - T.gofs[si]);
-                if (dd[j]) atomicAdd(&cnt[(dd[j] < 0 ? -dd[j] : dd[j]) - 1], 1u);
-            }
-        }
-        __syncthreads();
-        // exclusive starts of the buckets (Hillis-Steele over 256 counters)
-        const uint32_t mine = cnt[t];
-        off[t] = mine;
-        for (uint32_t d = 1; d < SMSM_HALF; d <<= 1) {
-            __syncthreads();
-            const uint32_t a = t >= d ? off[t - d] : 0u;
-            __syncthreads();
-            off[t] += a;
-        }
-        __syncthreads();
-        const uint32_t start = off[t] - mine;
-        __syncthreads();
-        off[t] = start;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            if (dd[j]) {
-                const uint32_t b = (dd[j] < 0 ? -dd[j] : dd[j]) - 1;
-                list[atomicAdd(&off[b], 1u)] = loc[j] | (dd[j] < 0 ? 0x80000000u : 0u);
-            }
-        }
-        __syncthreads();
-        // bucket t: its points of this tile, the next one in flight
-        if (mine) {
-            BT p;
-            uint32_t v = list[start];
-            msm_load_base<FMT, NEGC>(p, sptr, v);
-            for (uint32_t k = 0; k < mine; k++) {
-                BT use = p;
-                const uint32_t cur = v;
-                if (k + 1 < mine) { v = list[start + k + 1]; msm_load_base<FMT, NEGC>(p, sptr, v); }
-                if (real) msm_add_loaded<NEGC>(acc, use, cur >> 31);
-                else { msm_init_loaded<NEGC>(acc, use, cur >> 31); real = true; }
-            }
-        }
-        __syncthreads();
-    }
-    // R = sum_t (t+1) S_t = sum_t suf_t, suf_t = sum_{u >= t} S_u
-    ge_store(&sh[t], acc);
-    for (uint32_t d = 1; d < SMSM_HALF; d <<= 1) {
-        __syncthreads();
-        ge a, b;
-        const bool act = t + d < SMSM_HALF;
-        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
-        __syncthreads();
-        if (act) ge_store(&sh[t], a);
-    }
-    for (uint32_t h = SMSM_HALF / 2; h >= 1; h >>= 1) {
-        __syncthreads();
-        if (t < h) {
-            ge a, b;
-            ge_load(a, &sh[t]); ge_load(b, &sh[t + h]);
-            ge_add(a, a, b);
-            ge_store(&sh[t], a);
-        }
-    }
-    if (t == 0) {
-        ge r; ge_load(r, &sh[0]);
-        ge_store(rows_out + row_perm(row, nmsm, SMSM_W), r);
-    }
-}
-
-static int msm_window(uint64_t total) {
+// Window width: lg(points) - 3 (measured best, profiles/r01 MSM window
+// sweeps), unless a GF(p)-multiply count of the job says another width in
+// [4, 16] needs 3% fewer: W entries per point (7M Niels / 8M cached madd)
+// against 2 nmsm W 2^(c-1) bucket additions (9M each). Widths above 16 would
+// add a third sort pass. E.g. the IPP's 2^19-point jobs of rounds 2-4 take
+// c = 15 (17 windows of 16384 buckets) instead of 16 (16 of 32768).
+static int msm_window(uint64_t total, int nmsm, int fmt) {
     int lg = 0;
     while ((1ULL << (lg + 1)) <= total) lg++;
-    int c = lg - 3;   // lg(points) - 3 (measured best, profiles/r01 MSM window sweeps)
+    int c = lg - 3;
     if (c < 4) c = 4;
     if (c > 16) c = 16;
-    return c;
+    const double madd = fmt == MSM_NIELS ? 7.0 : 8.0;
+    auto cost = [&](int w) {
+        const double W = (254 + w - 1) / w;
+        return W * (double)total * madd + 2.0 * nmsm * W * (double)(1u << (w - 1)) * 9.0;
+    };
+    static const bool model = [] { const char *e = getenv("BPG_MSM_WINDOW_MODEL"); return !e || e[0] != '0'; }();
+    int best = c;
+    for (int w = 4; w <= 16; w++)
+        if (cost(w) < cost(best)) best = w;
+    return model && cost(best) < 0.97 * cost(c) ? best : c;
 }
 
 MsmEngine::~MsmEngine() {
@@ -1295,7 +1208,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     if (total > 0x7fffffffu) throw HipError(hipErrorInvalidValue, "msm job too large", __FILE__, __LINE__);
     T.gofs[nseg] = (uint32_t)total;
     p.total = total;
-    p.c = msm_window(total);
+    p.c = msm_window(total, nmsm, fmt);
     p.W = (254 + p.c - 1) / p.c;
     p.nmsm = nmsm;
     p.rows = nmsm * p.W;
@@ -1323,38 +1236,6 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         negc = negc && segs[i].negofs != 0;
         T.row0[i] = segs[i].msm;
     }
-    static const uint32_t smsm_max = [] {
-        const char *e = getenv("BPG_SMALL_MSM");
-        return e ? (uint32_t)atol(e) : (uint32_t)SMSM_MAX;
-    }();
-    if (total > 0 && total <= smsm_max && nmsm <= 4) {   // small job: two launches (k_smsm_*)
-        p.c = SMSM_C;
-        p.W = SMSM_W;
-        p.rows = nmsm * p.W;
-        p.half = SMSM_HALF;
-        p.E0 = (uint64_t)p.W * total;
-        p.passes = 0;
-        keys_.grow((size_t)p.W * total * sizeof(int16_t) + 256);
-        rows_dev_.grow((size_t)p.rows * sizeof(ge));
-        int16_t *dig = reinterpret_cast<int16_t *>(keys_.p);
-        SmsmRows R{};
-        for (int m = 0; m < nmsm; m++) { R.moff[m] = moff[m]; R.mtot[m] = mtot[m]; }
-        ProfScope ps(fmt == MSM_CACHED ? "msm_small_cached" : "msm_small_niels", 96.0 * (double)total,
-                     (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0);
-        hipLaunchKernelGGL(k_smsm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, dig);
-        if (fmt == MSM_NIELS && negc)
-            hipLaunchKernelGGL((k_smsm_rows<MSM_NIELS, true>), dim3(p.rows), dim3(SMSM_HALF), 0, st_, T, dig,
-                               (uint32_t)total, (uint32_t)nmsm, R, AS_GE(rows_dev_.p));
-        else if (fmt == MSM_NIELS)
-            hipLaunchKernelGGL((k_smsm_rows<MSM_NIELS, false>), dim3(p.rows), dim3(SMSM_HALF), 0, st_, T, dig,
-                               (uint32_t)total, (uint32_t)nmsm, R, AS_GE(rows_dev_.p));
-        else
-            hipLaunchKernelGGL((k_smsm_rows<MSM_CACHED, false>), dim3(p.rows), dim3(SMSM_HALF), 0, st_, T, dig,
-                               (uint32_t)total, (uint32_t)nmsm, R, AS_GE(rows_dev_.p));
-        BPG_HIP(hipGetLastError());
-        BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
-        return p;
-    }
     p.E0 = (uint64_t)p.W * total;
     p.T = RBK_T;
     // keys: row << c | slot (slot <= half, half = trash); padding key = rows << c
@@ -1376,40 +1257,58 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     // sort tiles: each row's contiguous entries cut into tiles of at most `tile`
     uint64_t tile = (p.E0 + 2047) / 2048;
     tile = std::max<uint64_t>(RS_ITER, (tile + RS_ITER - 1) / RS_ITER * RS_ITER);
-    if (!tiles_ev_) {
-        BPG_HIP(hipEventCreateWithFlags(&tiles_ev_, hipEventDisableTiming));
-        // tile table (5 words per tile), then each row's first tile
-        BPG_HIP(hipHostMalloc((void **)&tiles_host_, (size_t)6 * RS_MAXTILES * 4, hipHostMallocDefault));
-        tiles_.grow((size_t)6 * RS_MAXTILES * 4);
-    } else {
-        event_wait(tiles_ev_);   // the previous job's upload has left the staging buffer
-    }
-    uint32_t nt = 0;
-    std::vector<uint32_t> rowfirst(p.rows);
-    for (int r = 0; r < p.rows; r++) {
-        const uint32_t m = (uint32_t)r % nmsm, w = (uint32_t)r / nmsm;
-        const uint64_t rs = (uint64_t)w * total + moff[m];
-        const uint64_t rn = mtot[m];
-        const uint32_t t0 = nt;
-        for (uint64_t a = 0; a < rn; a += tile) {
-            if (nt >= RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
-            uint32_t *e = tiles_host_ + 5 * nt++;
-            e[0] = (uint32_t)(rs + a); e[1] = (uint32_t)(rs + std::min<uint64_t>(rn, a + tile));
-            e[4] = (uint32_t)rs;
-        }
-        for (uint32_t k = t0; k < nt; k++) { tiles_host_[5 * k + 2] = t0; tiles_host_[5 * k + 3] = nt; }
-        rowfirst[r] = t0;
-    }
-    if (nt + p.rows > RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
-    memcpy(tiles_host_ + 5 * nt, rowfirst.data(), (size_t)p.rows * 4);
-    BPG_HIP(hipMemcpyAsync(tiles_.p, tiles_host_, (size_t)(5 * nt + p.rows) * 4, hipMemcpyHostToDevice, st_));
-    BPG_HIP(hipEventRecord(tiles_ev_, st_));
-    uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
+    tiles_.grow((size_t)6 * RS_MAXTILES * 4);
     uint8_t *bflag = (uint8_t *)bflag_.p;
+    TileGeo geo{};
+    geo.rows = (uint32_t)p.rows;
+    geo.tile = (uint32_t)tile;
+    geo.bflag = bflag;
+    geo.bflag_bytes = (D + 15) / 16 * 16;   // bflag_ holds D + D/4 + 256 bytes
+    uint32_t nt = 0;
+    if (nmsm <= 4) {   // the digit launch writes the tile table
+        for (int m = 0; m < nmsm; m++) {
+            geo.moff[m] = moff[m];
+            geo.mtot[m] = mtot[m];
+            geo.tpr[m] = (uint32_t)((mtot[m] + tile - 1) / tile);
+            geo.cum[m] = geo.TW;
+            geo.TW += geo.tpr[m];
+        }
+        nt = (uint32_t)p.W * geo.TW;
+        geo.nt = nt;
+        geo.tiles = (uint32_t *)tiles_.p;
+        if (nt + p.rows > RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
+    } else {
+        if (!tiles_ev_) {
+            BPG_HIP(hipEventCreateWithFlags(&tiles_ev_, hipEventDisableTiming));
+            // tile table (5 words per tile), then each row's first tile
+            BPG_HIP(hipHostMalloc((void **)&tiles_host_, (size_t)6 * RS_MAXTILES * 4, hipHostMallocDefault));
+        } else {
+            event_wait(tiles_ev_);   // the previous job's upload has left the staging buffer
+        }
+        std::vector<uint32_t> rowfirst(p.rows);
+        for (int r = 0; r < p.rows; r++) {
+            const uint32_t m = (uint32_t)r % nmsm, w = (uint32_t)r / nmsm;
+            const uint64_t rs = (uint64_t)w * total + moff[m];
+            const uint64_t rn = mtot[m];
+            const uint32_t t0 = nt;
+            for (uint64_t a = 0; a < rn; a += tile) {
+                if (nt >= RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
+                uint32_t *e = tiles_host_ + 5 * nt++;
+                e[0] = (uint32_t)(rs + a); e[1] = (uint32_t)(rs + std::min<uint64_t>(rn, a + tile));
+                e[4] = (uint32_t)rs;
+            }
+            for (uint32_t k = t0; k < nt; k++) { tiles_host_[5 * k + 2] = t0; tiles_host_[5 * k + 3] = nt; }
+            rowfirst[r] = t0;
+        }
+        if (nt + p.rows > RS_MAXTILES) throw HipError(hipErrorInvalidValue, "sort tiles", __FILE__, __LINE__);
+        memcpy(tiles_host_ + 5 * nt, rowfirst.data(), (size_t)p.rows * 4);
+        BPG_HIP(hipMemcpyAsync(tiles_.p, tiles_host_, (size_t)(5 * nt + p.rows) * 4, hipMemcpyHostToDevice, st_));
+        BPG_HIP(hipEventRecord(tiles_ev_, st_));
+    }
+    uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     ge *buckets = AS_GE(buckets_.p);
-    BPG_HIP(hipMemsetAsync(bflag, 0, D, st_));
     hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
-                       (uint32_t)nmsm, (uint32_t)p.half, keys, vals);
+                       (uint32_t)nmsm, (uint32_t)p.half, keys, vals, geo);
     BPG_HIP(hipGetLastError());
     radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt,
                (const uint32_t *)tiles_.p + 5 * nt, (uint32_t)p.rows, (uint32_t *)sort_tmp_.p,

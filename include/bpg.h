@@ -102,7 +102,12 @@ int bpg_set_device(int device);
  * set, the first process derives and writes `bpg_gens_<N>.bin` there and
  * later processes load it (checked by a checksum and by recomputing the
  * first points of both chains). NULL or "" turns the cache off; default:
- * env BPG_GENS_CACHE, else off. */
+ * env BPG_GENS_CACHE, else off. The directory must be TRUSTED: a file is
+ * loaded only if owned by the effective uid and not group/other-writable,
+ * in a directory owned by that uid (or root) that group/others cannot
+ * write; and only provers use a loaded set — every verifier entry point
+ * re-derives the generators, since a planted set with known discrete-log
+ * relations would make forged proofs verify. */
 void bpg_gens_cache_dir(const char *dir);
 
 /* ------------------------------------------------------------------------ */
