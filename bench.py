@@ -91,6 +91,21 @@ def pmc_row(kernel):
     return row
 
 
+def prof_row(kernel):
+    """The average duration (us) and launch count of `kernel` in the latest
+    committed rocprofv3 --kernel-trace --stats table of the default 24-thread
+    bench (profiles/*_prof24_kernels.md, scripts/prof_summary.py), or {}."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_prof24_kernels.md")))
+    if not files:
+        return {}
+    for line in open(files[-1]):
+        cells = [c.strip() for c in line.strip().strip("|").split("|")]
+        if len(cells) >= 4 and cells[0].replace("void ", "") == kernel:
+            return {"avg_us": float(cells[3]), "calls": int(cells[1]), "source": os.path.relpath(files[-1], ROOT)}
+    return {}
+
+
 def _cpu_sample(leaves):
     """(constraints, seconds) of one warm single-thread oracle proof of the
     config-5 family with `leaves` Merkle leaves (also run as a child process
@@ -423,6 +438,7 @@ def main():
         sec = ms / lc / 1e3                      # average launch duration
         achieved = (by / lc) / sec / 1e9         # GB/s of algorithmic bytes
         pmc = pmc_row(KERNELS[dom])
+        prof = prof_row(KERNELS[dom])
         roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm",
                 # the HBM fraction is the metric's; the kernel is limited by its
                 # GF(p) multiply rate and gather latency, see "valu"
@@ -440,6 +456,11 @@ def main():
                 "pmc_isolated": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()
                                  if k in ("avg_us", "valu_issue_share", "avg_waves_per_simd", "wave_wait_mem",
                                           "hbm_gbs", "clock_ghz", "source")} or None,
+                # the same kernel's average launch in the committed rocprofv3
+                # kernel trace of this command (24 host threads), and the HBM
+                # fraction that average gives
+                "rocprof_24threads": dict(prof, frac=round((by / lc) / (prof["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 6))
+                if prof else None,
                 "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
                 "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items() if v}}
 

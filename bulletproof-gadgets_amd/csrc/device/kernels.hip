@@ -1076,8 +1076,8 @@ __global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ blkB, c
 }
 
 // Window width: lg(points) - 3 (measured best, profiles/r01 MSM window
-// sweeps), unless a GF(p)-multiply count of the job says another width in
-// [4, 16] needs 3% fewer: W entries per point (7M Niels / 8M cached madd)
+// sweeps). With BPG_MSM_WINDOW_MODEL=1, another width in [4, 16] when a
+// GF(p)-multiply count of the job says it needs 3% fewer: W entries per point (7M Niels / 8M cached madd)
 // against 2 nmsm W 2^(c-1) bucket additions (9M each). Widths above 16 would
 // add a third sort pass. E.g. the IPP's 2^19-point jobs of rounds 2-4 take
 // c = 15 (17 windows of 16384 buckets) instead of 16 (16 of 32768).
@@ -1092,7 +1092,10 @@ static int msm_window(uint64_t total, int nmsm, int fmt) {
         const double W = (254 + w - 1) / w;
         return W * (double)total * madd + 2.0 * nmsm * W * (double)(1u << (w - 1)) * 9.0;
     };
-    static const bool model = [] { const char *e = getenv("BPG_MSM_WINDOW_MODEL"); return !e || e[0] != '0'; }();
+    // off by default: 74.0 / 74.6 vs 74.4 / 75.0 M constraints/s without it
+    // (profiles/r03d_ab_window_model_threads.txt) — the chip is VALU-bound,
+    // the extra window's additions cost more than the smaller bucket rows save
+    static const bool model = [] { const char *e = getenv("BPG_MSM_WINDOW_MODEL"); return e && e[0] == '1'; }();
     int best = c;
     for (int w = 4; w <= 16; w++)
         if (cost(w) < cost(best)) best = w;

@@ -398,6 +398,12 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
             if (v >= 1 && (uint32_t)v < threads) P = std::min<uint32_t>(groups, (uint32_t)v);
         }
         uint32_t C = std::max<uint32_t>(1, std::min<uint32_t>(count, threads > P ? threads - P : 1));
+        // proofs per consumer step (BPG_LOCKSTEP, 1 or 2)
+        static const int lockstep = [] {
+            const char *e = getenv("BPG_LOCKSTEP");
+            const int v = e ? atoi(e) : 1;
+            return v >= 2 ? 2 : 1;
+        }();
         uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
         std::vector<uint8_t *> slot = cs.slots(nslots, 2 * (size_t)cs.n * 64 + 64);
         std::mutex mu;
@@ -451,21 +457,33 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                     producers_left--;
                     cv.notify_all();
                 } else {
+                    // each consumer proves up to `lockstep` ready proofs at once
+                    // on its stream (gpu_prove_lockstep: one MSM job per step
+                    // for all of them)
                     for (;;) {
-                        uint32_t k;
+                        uint32_t ks[2];
+                        int nk = 0;
                         {
                             std::unique_lock<std::mutex> lk(mu);
                             cv.wait(lk, [&] { return abort || !ready.empty() || producers_left == 0; });
                             if (abort || ready.empty()) break;
-                            k = ready.front();
-                            ready.pop_front();
+                            while (!ready.empty() && nk < lockstep) {
+                                ks[nk++] = ready.front();
+                                ready.pop_front();
+                            }
                         }
-                        std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, blocks[k], &timings[k]);
-                        if (pr.size() > proof_stride) throw std::runtime_error("proof stride too small");
-                        memcpy(proof_out + proof_stride * (size_t)k, pr.data(), pr.size());
-                        lens[k] = pr.size();
+                        const RngBlock *rbs[2];
+                        ProveTimings tms[2];
+                        for (int i = 0; i < nk; i++) rbs[i] = &blocks[ks[i]];
+                        std::vector<std::vector<uint8_t>> prs = gpu_prove_lockstep(cs, label, label_len, rbs, nk, tms);
+                        for (int i = 0; i < nk; i++) {
+                            if (prs[i].size() > proof_stride) throw std::runtime_error("proof stride too small");
+                            memcpy(proof_out + proof_stride * (size_t)ks[i], prs[i].data(), prs[i].size());
+                            lens[ks[i]] = prs[i].size();
+                            timings[ks[i]] = tms[i];
+                        }
                         std::lock_guard<std::mutex> lk(mu);
-                        free_slots.push_back(slot_of[k]);
+                        for (int i = 0; i < nk; i++) free_slots.push_back(slot_of[ks[i]]);
                         cv.notify_all();
                     }
                 }

@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <map>
@@ -314,20 +315,37 @@ bool get_kernel_stat(const char *name, KernelStat &out) {
 void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_stats.clear(); }
 
 // ---------------------------------------------------------------- workspace
+// Per-proof device buffers of the prover: a workspace drives up to
+// MAX_LOCKSTEP proofs of one circuit in lockstep (gpu_prove_lockstep).
+static const int MAX_LOCKSTEP = 2;
+static const size_t ROWS_HALF = 1024;   // pinned MSM row buffer: commitments [0, 1024), IPP L/R [1024, 2048)
+struct ProofBufs {
+    DBuf wide, sL, sR, w, wloc, l1, r0, r1, r3, ypm, yipm, zlo, zhi, ylo, yhi, tabs, a, b, mscal, partial, Gp[2], Hp[2],
+        small, wG, wH, wconv, f3tab;
+    ScD *small_host = nullptr;   // pinned, 4096 scalars
+    dev::ArgStage fold_stage, comb_stage, fold2_stage, fold3_stage;
+    ~ProofBufs() {
+        for (dev::ArgStage *a : {&fold_stage, &comb_stage, &fold2_stage, &fold3_stage}) {
+            if (a->dev) (void)hipFree(a->dev);
+            if (a->host) (void)hipHostFree(a->host);
+            if (a->copied) (void)hipEventDestroy(a->copied);
+        }
+        if (small_host) (void)hipHostFree(small_host);
+        DBuf *bufs[] = {&wide, &sL, &sR, &w, &wloc, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs,
+                        &a, &b, &mscal, &partial, &Gp[0], &Gp[1], &Hp[0], &Hp[1], &small, &wG, &wH, &wconv, &f3tab};
+        for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
+    }
+};
 struct Workspace : dev::ProfSink {
+    ProofBufs pb[MAX_LOCKSTEP];      // the prover's per-proof buffers (the verifier uses the ones below)
     int device = 0;
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
-    DBuf wide, sL, sR, w, l1, r0, r1, r3, ypm, yipm, zlo, zhi, tabs, a, b, mscal, partial, Gp[2], Hp[2], Q, small, gh,
-        ynwR, pts, okflag, wG, wH, wloc, wconv, f3tab;
-    PtD *rows_host = nullptr;        // pinned, 8 x 64 rows
+    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag;
+    PtD *rows_host = nullptr;        // pinned, 2 x ROWS_HALF window rows
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
-    dev::ArgStage fold_stage;        // IPP fold kernel arguments
-    dev::ArgStage comb_stage;        // table-fold kernel arguments
-    dev::ArgStage fold2_stage;       // two-round Straus fold kernel arguments
-    dev::ArgStage fold3_stage;       // three-round Straus fold kernel arguments
     hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
     void sync() {
         BPG_HIP(hipEventRecord(done_ev, st));
@@ -336,22 +354,10 @@ struct Workspace : dev::ProfSink {
     ~Workspace() {
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (done_ev) (void)hipEventDestroy(done_ev);
-        if (fold_stage.dev) (void)hipFree(fold_stage.dev);
-        if (fold_stage.host) (void)hipHostFree(fold_stage.host);
-        if (fold_stage.copied) (void)hipEventDestroy(fold_stage.copied);
-        if (comb_stage.dev) (void)hipFree(comb_stage.dev);
-        if (comb_stage.host) (void)hipHostFree(comb_stage.host);
-        if (comb_stage.copied) (void)hipEventDestroy(comb_stage.copied);
-        for (dev::ArgStage *a : {&fold2_stage, &fold3_stage}) {
-            if (a->dev) (void)hipFree(a->dev);
-            if (a->host) (void)hipHostFree(a->host);
-            if (a->copied) (void)hipEventDestroy(a->copied);
-        }
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
-        DBuf *bufs[] = {&wide, &sL, &sR, &w, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &tabs, &a, &b, &mscal, &partial,
-                        &Gp[0], &Gp[1], &Hp[0], &Hp[1], &Q, &small, &gh, &ynwR, &pts, &okflag, &wG, &wH, &wloc, &wconv, &f3tab};
+        DBuf *bufs[] = {&w, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs, &mscal, &partial, &small, &gh, &ynwR, &pts, &okflag};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -414,7 +420,7 @@ Workspace &thread_workspace(int device) {
         BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
         BPG_HIP(hipEventCreateWithFlags(&p->done_ev, hipEventBlockingSync | hipEventDisableTiming));
         p->msm.reset(new MsmEngine(p->st));
-        BPG_HIP(hipHostMalloc((void **)&p->rows_host, 8 * 64 * sizeof(PtD), hipHostMallocDefault));
+        BPG_HIP(hipHostMalloc((void **)&p->rows_host, 2 * ROWS_HALF * sizeof(PtD), hipHostMallocDefault));
         BPG_HIP(hipHostMalloc((void **)&p->small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
     }
     dev::set_prof_sink(p.get());   // this thread's launches record on its own stream
@@ -611,26 +617,31 @@ int gpu_msm(int device, const uint8_t *scalars, const uint8_t *points, uint32_t 
     return 0;
 }
 
-// Upload base^(2^b) (b < 40) in Montgomery form; returns device pointer.
-static ScD *upload_base2(Workspace &ws, int slot, const Scalar &base) {
-    ScD *h = ws.small_host + 40 * slot;
+// Upload base^(2^b) (b < 40) in Montgomery form through the pinned slot
+// `slot` of small_host; returns the device pointer (in tabs).
+static ScD *upload_base2(ScD *small_host, DBuf &tabs, hipStream_t st, int slot, const Scalar &base) {
+    ScD *h = small_host + 40 * slot;
     Scalar cur = base;
     for (int b = 0; b < 40; b++) { h[b] = mont(cur); cur = cur * cur; }
-    ScD *d = as<ScD>(ws.tabs) + 40 * slot;
-    BPG_HIP(hipMemcpyAsync(d, h, 40 * sizeof(ScD), hipMemcpyHostToDevice, ws.st));
+    ScD *d = as<ScD>(tabs) + 40 * slot;
+    BPG_HIP(hipMemcpyAsync(d, h, 40 * sizeof(ScD), hipMemcpyHostToDevice, st));
     return d;
 }
 // out[i] = mont(mult * base^i), i < count, via two 1024-ary levels
-static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t count, DBuf &lo, DBuf &hi, ScD *out,
-                       const Scalar &mult = Scalar::one()) {
+static void pow_vector(ScD *small_host, DBuf &tabs, hipStream_t st, int slot, const Scalar &base, uint32_t count,
+                       DBuf &lo, DBuf &hi, ScD *out, const Scalar &mult = Scalar::one()) {
     uint32_t nhi = count / 1024 + 1;
     lo.grow(1024 * sizeof(ScD));
     hi.grow((size_t)nhi * sizeof(ScD));
-    ScD *b2 = upload_base2(ws, slot, base);
-    ScD *b2h = upload_base2(ws, slot + 1, sc_pow_u64(base, 1024));
-    launch_pow_table(b2, 0, 1024, as<ScD>(lo), ws.st);
-    launch_pow_table(b2h, 0, nhi, as<ScD>(hi), ws.st);
-    if (out) launch_pow_expand(as<ScD>(lo), as<ScD>(hi), count, mont(mult), out, ws.st);
+    ScD *b2 = upload_base2(small_host, tabs, st, slot, base);
+    ScD *b2h = upload_base2(small_host, tabs, st, slot + 1, sc_pow_u64(base, 1024));
+    launch_pow_table(b2, 0, 1024, as<ScD>(lo), st);
+    launch_pow_table(b2h, 0, nhi, as<ScD>(hi), st);
+    if (out) launch_pow_expand(as<ScD>(lo), as<ScD>(hi), count, mont(mult), out, st);
+}
+static void pow_vector(Workspace &ws, int slot, const Scalar &base, uint32_t count, DBuf &lo, DBuf &hi, ScD *out,
+                       const Scalar &mult = Scalar::one()) {
+    pow_vector(ws.small_host, ws.tabs, ws.st, slot, base, count, lo, hi, out, mult);
 }
 
 // ------------------------------------------------------------------- prove
@@ -867,203 +878,210 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
     return out;
 }
 
-std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
-                                   ProveTimings *tm, const AllGather *ag) {
+// Prover::prove (prove.rs:79) after the RNG phase for P proofs of one
+// prepared circuit in lockstep on this thread's stream (P = 1: the single
+// proof; the sharded prover). The proofs share the circuit, so their control
+// flow (round groups, tail, lane classes) is identical and only scalars,
+// transcripts and buffers differ: every MSM job covers all P proofs (one
+// digit/sort/run-reduction/bucket chain of latency-bound launches for P
+// proofs, 2P or 3P MSMs), the other kernels run per proof (ProofBufs).
+// The IPP's c_L Q and c_R Q terms are added on the host (Q = w B, so
+// c Q = (c w) B by the fixed-base table): the L/R jobs hold only generator
+// segments (at most 16 per proof, 32 per job).
+std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
+                                                     const RngBlock *const *rbs, int P, ProveTimings *tms,
+                                                     const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
+    if (P < 1 || P > MAX_LOCKSTEP) throw std::runtime_error("lockstep proof count");
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t n = cs.n, m = cs.m, N = cs.N, lgN = cs.lgN;
     // this rank's slice: lanes i = j * world + rank, j < nl real, j < Nl padded
     const uint32_t world = cs.world, rank = cs.rank, nl = cs.nl, Nl = cs.Nl;
     const bool sharded = world > 1;
     if (sharded && !ag) throw std::runtime_error("sharded prove without an exchange");
+    if (sharded && P != 1) throw std::runtime_error("the sharded prover proves one proof at a time");
     std::shared_ptr<const GenSet> gs = ctx.gens(N, rank, world);
     Workspace &ws = thread_workspace(cs.device);
     hipStream_t st = ws.st;
     double t0 = now_ms();
-    ws.tabs.grow(8 * 40 * sizeof(ScD));
-    Transcript T = prover_transcript(cs, label, label_len);
-    const Scalar i_bl = rb.i_bl, o_bl = rb.o_bl, s_bl = rb.s_bl;
+    std::vector<Transcript> T;
+    for (int p = 0; p < P; p++) {
+        ProofBufs &B = ws.pb[p];
+        B.tabs.grow(8 * 40 * sizeof(ScD));
+        if (!B.small_host) BPG_HIP(hipHostMalloc((void **)&B.small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
+        T.push_back(prover_transcript(cs, label, label_len));
+    }
 
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G>, S1 = <s_L,G> + <s_R,H>
-    // (blinding terms added on the host): one MSM job of three MSMs, or
-    // (COMMIT_ONE_JOB=0) A_I1/A_O1 and S1 as two jobs
-    PtD *rowsA = ws.rows_host, *rowsS = ws.rows_host + 128, *rowsLR = ws.rows_host + 256;
-    MsmPlan pA{}, pS{};
+    // (blinding terms added on the host): one MSM job, MSMs 3p .. 3p + 2
+    PtD *rowsA = ws.rows_host, *rowsLR = ws.rows_host + ROWS_HALF;
     const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
     const int64_t gneg = gs->N;             // their negations follow each vector
-    static const bool one_job = [] { const char *e = getenv("BPG_COMMIT_ONE_JOB"); return !e || e[0] != '0'; }();
-    const MsmSeg segA[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg},
-                            {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg},
-                            {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg}};
-    if (nl && !one_job) {
-        int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
-        pA = ws.msm->enqueue(segA, 3, 2, rowsA, MSM_NIELS);
-        ws.prof_end(ph);
-    }
-    // s_L | s_R: raw 64-byte draws -> device, reduced mod l there (this
-    // rank's lanes only)
-    ws.sL.grow((size_t)nl * sizeof(ScD) + 64);
-    ws.sR.grow((size_t)nl * sizeof(ScD) + 64);
-    if (nl) {
-        const uint8_t *wd = rb.wide;
-        if (!rb.on_device) {
-            ws.wide.grow(2 * (size_t)n * 64 + 64);
-            BPG_HIP(hipMemcpyAsync(ws.wide.p, rb.wide, 2 * (size_t)n * 64, hipMemcpyHostToDevice, st));
-            wd = as<uint8_t>(ws.wide);
+    MsmPlan pA{};
+    {
+        MsmSeg seg[5 * MAX_LOCKSTEP];
+        int nseg = 0;
+        for (int p = 0; p < P; p++) {
+            ProofBufs &B = ws.pb[p];
+            const RngBlock &rb = *rbs[p];
+            // s_L | s_R: raw 64-byte draws -> device, reduced mod l there (this
+            // rank's lanes only)
+            B.sL.grow((size_t)nl * sizeof(ScD) + 64);
+            B.sR.grow((size_t)nl * sizeof(ScD) + 64);
+            if (!nl) continue;
+            const uint8_t *wd = rb.wide;
+            if (!rb.on_device) {
+                B.wide.grow(2 * (size_t)n * 64 + 64);
+                BPG_HIP(hipMemcpyAsync(B.wide.p, rb.wide, 2 * (size_t)n * 64, hipMemcpyHostToDevice, st));
+                wd = as<uint8_t>(B.wide);
+            }
+            launch_wide_reduce(wd, nl, world, rank, as<ScD>(B.sL), st);
+            launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(B.sR), st);
+            const uint32_t m0 = 3 * (uint32_t)p;
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, m0, gneg};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, m0, gneg};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, m0 + 1, gneg};
+            seg[nseg++] = {as<ScD>(B.sL), G0, nl, m0 + 2, gneg};
+            seg[nseg++] = {as<ScD>(B.sR), H0, nl, m0 + 2, gneg};
         }
-        launch_wide_reduce(wd, nl, world, rank, as<ScD>(ws.sL), st);
-        launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(ws.sR), st);
-        if (one_job) {
-            const MsmSeg seg[5] = {segA[0], segA[1], segA[2], {as<ScD>(ws.sL), G0, nl, 2, gneg},
-                                   {as<ScD>(ws.sR), H0, nl, 2, gneg}};
-            int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
-            pA = ws.msm->enqueue(seg, 5, 3, rowsA, MSM_NIELS);
-            ws.prof_end(ph);
-        } else {
-            MsmSeg segS[2] = {{as<ScD>(ws.sL), G0, nl, 0, gneg}, {as<ScD>(ws.sR), H0, nl, 0, gneg}};
-            int ph = ws.prof_begin("msm_commit", 2.0 * nl * (64 + 32));
-            pS = ws.msm->enqueue(segS, 2, 1, rowsS, MSM_NIELS);
+        if (nseg) {
+            int ph = ws.prof_begin("msm_commit", 5.0 * P * nl * (64 + 32));
+            pA = ws.msm->enqueue(seg, nseg, 3 * P, rowsA, MSM_NIELS);
             ws.prof_end(ph);
         }
     }
     ws.sync();
-    Point AIS[3], tmp;
-    if (nl) {
-        combine_rows(AIS[0], rowsA, pA.W, pA.c);
-        combine_rows(AIS[1], rowsA + pA.W, pA.W, pA.c);
-        if (one_job) combine_rows(AIS[2], rowsA + 2 * pA.W, pA.W, pA.c);
-        else combine_rows(AIS[2], rowsS, pS.W, pS.c);
-    } else {
-        pt_identity(AIS[0]); pt_identity(AIS[1]); pt_identity(AIS[2]);
+    std::vector<Scalar> y(P), z(P);
+    std::vector<std::array<uint8_t, 96>> cA(P);   // compressed A_I1 | A_O1 | S1
+    for (int p = 0; p < P; p++) {
+        const RngBlock &rb = *rbs[p];
+        Point AIS[3], tmp;
+        if (nl) {
+            for (int k = 0; k < 3; k++) combine_rows(AIS[k], rowsA + (3 * p + k) * pA.W, pA.W, pA.c);
+        } else {
+            pt_identity(AIS[0]); pt_identity(AIS[1]); pt_identity(AIS[2]);
+        }
+        if (sharded) {
+            std::vector<Point> sum = allgather_point_sums(*ag, AIS, 3, world);
+            for (int k = 0; k < 3; k++) AIS[k] = sum[k];
+        }
+        mul_B_blinding(tmp, rb.i_bl); pt_add(AIS[0], AIS[0], tmp);
+        mul_B_blinding(tmp, rb.o_bl); pt_add(AIS[1], AIS[1], tmp);
+        mul_B_blinding(tmp, rb.s_bl); pt_add(AIS[2], AIS[2], tmp);
+        uint8_t *c = cA[p].data();
+        ristretto_compress(c, AIS[0]); ristretto_compress(c + 32, AIS[1]); ristretto_compress(c + 64, AIS[2]);
+        T[p].append_point("A_I1", c);
+        T[p].append_point("A_O1", c + 32);
+        T[p].append_point("S1", c + 64);
+        T[p].append_message("dom-sep", (const uint8_t *)"r1cs-1phase", 11);
+        const uint8_t zero32[32] = {0};
+        T[p].append_point("A_I2", zero32);
+        T[p].append_point("A_O2", zero32);
+        T[p].append_point("S2", zero32);
+        y[p] = T[p].challenge_scalar("y");
+        z[p] = T[p].challenge_scalar("z");
     }
-    if (sharded) {
-        std::vector<Point> sum = allgather_point_sums(*ag, AIS, 3, world);
-        for (int k = 0; k < 3; k++) AIS[k] = sum[k];
-    }
-    Point &AI = AIS[0], &AO = AIS[1], &S = AIS[2];
-    mul_B_blinding(tmp, i_bl); pt_add(AI, AI, tmp);
-    mul_B_blinding(tmp, o_bl); pt_add(AO, AO, tmp);
-    mul_B_blinding(tmp, s_bl); pt_add(S, S, tmp);
-    uint8_t cAI[32], cAO[32], cS[32];
-    ristretto_compress(cAI, AI); ristretto_compress(cAO, AO); ristretto_compress(cS, S);
-    T.append_point("A_I1", cAI);
-    T.append_point("A_O1", cAO);
-    T.append_point("S1", cS);
-    T.append_message("dom-sep", (const uint8_t *)"r1cs-1phase", 11);
-    const uint8_t zero32[32] = {0};
-    T.append_point("A_I2", zero32);
-    T.append_point("A_O2", zero32);
-    T.append_point("S2", zero32);
-    Scalar y = T.challenge_scalar("y"), z = T.challenge_scalar("z");
     double t1 = now_ms();
 
     // vectors: powers, flattened_constraints(z), l(x)/r(x) coefficients, t(x)
     // (y^i and y^-i at this rank's lanes: (y^world)^j * y^rank)
-    Scalar y_inv = sc_invert(y);
-    ws.ypm.grow((size_t)Nl * sizeof(ScD));
-    ws.yipm.grow((size_t)Nl * sizeof(ScD));
-    DBuf &lo1 = ws.zlo, &hi1 = ws.zhi;
-    pow_vector(ws, 0, sharded ? sc_pow_u64(y, world) : y, Nl, lo1, hi1, as<ScD>(ws.ypm),
-               sharded ? sc_pow_u64(y, rank) : Scalar::one());
-    // second set of tables for y^-1 uses gh as temp space for the hi level
-    ws.gh.grow(std::max<size_t>((size_t)(N / 1024 + 2) * sizeof(ScD), 64));
-    {
-        DBuf lo2, hi2;
-        pow_vector(ws, 2, sharded ? sc_pow_u64(y_inv, world) : y_inv, Nl, lo2, hi2, as<ScD>(ws.yipm),
-                   sharded ? sc_pow_u64(y_inv, rank) : Scalar::one());
-        pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);   // also syncs tables below
-        ws.sync();
-        if (lo2.p) (void)hipFree(lo2.p);
-        if (hi2.p) (void)hipFree(hi2.p);
-    }
-    ws.w.grow((size_t)cs.ncol * sizeof(ScD) + 64);
+    std::vector<Scalar> y_inv(P);
     CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
                as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
                as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
-    int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32);
-    launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
-    ws.partial.grow(1024 * 8 * sizeof(ScD));
-    for (uint32_t col : cs.huge_cols)
-        launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(ws.zlo), as<ScD>(ws.zhi),
-                            as<ScD>(ws.partial), as<ScD>(ws.w), st);
-    ws.prof_end(pfl);
-    ScD *wfull = as<ScD>(ws.w);
-    ScD *wV = wfull + 3 * (size_t)n;
-    ScD *wL = wfull, *wR = wfull + n, *wO = wfull + 2 * (size_t)n;
-    if (sharded) {   // w_L, w_R, w_O at this rank's lanes
-        ws.wloc.grow(3 * (size_t)nl * sizeof(ScD) + 64);
-        wL = as<ScD>(ws.wloc); wR = wL + nl; wO = wL + 2 * (size_t)nl;
-        launch_gather_scalars(wfull, nl, world, rank, wL, st);
-        launch_gather_scalars(wfull + n, nl, world, rank, wR, st);
-        launch_gather_scalars(wfull + 2 * (size_t)n, nl, world, rank, wO, st);
+    for (int p = 0; p < P; p++) {
+        ProofBufs &B = ws.pb[p];
+        y_inv[p] = sc_invert(y[p]);
+        B.ypm.grow((size_t)Nl * sizeof(ScD));
+        B.yipm.grow((size_t)Nl * sizeof(ScD));
+        pow_vector(B.small_host, B.tabs, st, 0, sharded ? sc_pow_u64(y[p], world) : y[p], Nl, B.zlo, B.zhi,
+                   as<ScD>(B.ypm), sharded ? sc_pow_u64(y[p], rank) : Scalar::one());
+        // the y^-1 tables live in the workspace: a hipFree per proof would
+        // synchronise the whole device, every other stream included
+        pow_vector(B.small_host, B.tabs, st, 2, sharded ? sc_pow_u64(y_inv[p], world) : y_inv[p], Nl, B.ylo, B.yhi,
+                   as<ScD>(B.yipm), sharded ? sc_pow_u64(y_inv[p], rank) : Scalar::one());
+        pow_vector(B.small_host, B.tabs, st, 4, z[p], cs.q + 2, B.zlo, B.zhi, nullptr);
+        B.w.grow((size_t)cs.ncol * sizeof(ScD) + 64);
+        int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32);
+        launch_flatten(csc, as<ScD>(B.zlo), as<ScD>(B.zhi), as<ScD>(B.w), st);
+        B.partial.grow(1024 * 8 * sizeof(ScD));
+        for (uint32_t col : cs.huge_cols)
+            launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(B.zlo),
+                                as<ScD>(B.zhi), as<ScD>(B.partial), as<ScD>(B.w), st);
+        ws.prof_end(pfl);
+        ScD *wfull = as<ScD>(B.w);
+        ScD *wV = wfull + 3 * (size_t)n;
+        ScD *wL = wfull, *wR = wfull + n, *wO = wfull + 2 * (size_t)n;
+        if (sharded) {   // w_L, w_R, w_O at this rank's lanes
+            B.wloc.grow(3 * (size_t)nl * sizeof(ScD) + 64);
+            wL = as<ScD>(B.wloc); wR = wL + nl; wO = wL + 2 * (size_t)nl;
+            launch_gather_scalars(wfull, nl, world, rank, wL, st);
+            launch_gather_scalars(wfull + n, nl, world, rank, wR, st);
+            launch_gather_scalars(wfull + 2 * (size_t)n, nl, world, rank, wO, st);
+        }
+        for (DBuf *d : {&B.l1, &B.r0, &B.r1, &B.r3}) d->grow((size_t)nl * sizeof(ScD) + 64);
+        B.small.grow(64 * sizeof(ScD));
+        ScD *dsmall = as<ScD>(B.small);
+        if (nl) {
+            launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(B.sR), wL,
+                            wR, wO, as<ScD>(B.ypm), as<ScD>(B.yipm), nl, as<ScD>(B.l1), as<ScD>(B.r0), as<ScD>(B.r1),
+                            as<ScD>(B.r3), st);
+            launch_tpoly(as<ScD>(B.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(B.sL), as<ScD>(B.r0),
+                         as<ScD>(B.r1), as<ScD>(B.r3), nl, as<ScD>(B.partial), dsmall, st);
+        } else {
+            BPG_HIP(hipMemsetAsync(dsmall, 0, 6 * sizeof(ScD), st));
+        }
+        if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(B.partial), dsmall + 6, st);
+        else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
+        BPG_HIP(hipMemcpyAsync(B.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
     }
-    for (DBuf *d : {&ws.l1, &ws.r0, &ws.r1, &ws.r3}) d->grow((size_t)nl * sizeof(ScD) + 64);
-    ws.small.grow(64 * sizeof(ScD));
-    ScD *dsmall = as<ScD>(ws.small);
-    if (nl) {
-        launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(ws.sR), wL, wR,
-                        wO, as<ScD>(ws.ypm), as<ScD>(ws.yipm), nl, as<ScD>(ws.l1), as<ScD>(ws.r0), as<ScD>(ws.r1),
-                        as<ScD>(ws.r3), st);
-        launch_tpoly(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0),
-                     as<ScD>(ws.r1), as<ScD>(ws.r3), nl, as<ScD>(ws.partial), dsmall, st);
-    } else {
-        BPG_HIP(hipMemsetAsync(dsmall, 0, 6 * sizeof(ScD), st));
-    }
-    if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(ws.partial), dsmall + 6, st);
-    else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
-    BPG_HIP(hipMemcpyAsync(ws.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
     ws.sync();
-    Scalar tp[6];
-    for (int k = 0; k < 6; k++) tp[k] = from_dev(ws.small_host[1000 + k]);
-    if (sharded) {
-        std::vector<Scalar> sum = allgather_scalar_sums(*ag, tp, 6, world);
-        for (int k = 0; k < 6; k++) tp[k] = sum[k];
+    std::vector<Scalar> u(P), x(P), t_x(P), t_xb(P), e_bl(P), wch(P);
+    std::vector<std::array<uint8_t, 160>> cT(P);
+    for (int p = 0; p < P; p++) {
+        ProofBufs &B = ws.pb[p];
+        const RngBlock &rb = *rbs[p];
+        Scalar tp[6];
+        for (int k = 0; k < 6; k++) tp[k] = from_dev(B.small_host[1000 + k]);
+        if (sharded) {
+            std::vector<Scalar> sum = allgather_scalar_sums(*ag, tp, 6, world);
+            for (int k = 0; k < 6; k++) tp[k] = sum[k];
+        }
+        const Scalar tb2 = from_dev(B.small_host[1006]);   // <w_V, v_blinding>: every rank holds all of w_V
+        const Scalar tb1 = rb.tb[0], tb3 = rb.tb[1], tb4 = rb.tb[2], tb5 = rb.tb[3], tb6 = rb.tb[4];
+        uint8_t *c = cT[p].data();
+        pedersen_commit(c, tp[0], tb1);
+        pedersen_commit(c + 32, tp[2], tb3);
+        pedersen_commit(c + 64, tp[3], tb4);
+        pedersen_commit(c + 96, tp[4], tb5);
+        pedersen_commit(c + 128, tp[5], tb6);
+        T[p].append_point("T_1", c);
+        T[p].append_point("T_3", c + 32);
+        T[p].append_point("T_4", c + 64);
+        T[p].append_point("T_5", c + 96);
+        T[p].append_point("T_6", c + 128);
+        u[p] = T[p].challenge_scalar("u");
+        x[p] = T[p].challenge_scalar("x");
+        const Scalar xx = x[p];
+        auto eval6 = [&](const Scalar cc[6]) {
+            Scalar acc = xx * cc[5];
+            for (int k = 4; k >= 0; k--) acc = xx * (cc[k] + acc);
+            return acc;
+        };
+        const Scalar tbs[6] = {tb1, tb2, tb3, tb4, tb5, tb6};
+        t_x[p] = eval6(tp);
+        t_xb[p] = eval6(tbs);
+        e_bl[p] = xx * (rb.i_bl + xx * (rb.o_bl + xx * rb.s_bl));
+        T[p].append_scalar("t_x", t_x[p]);
+        T[p].append_scalar("t_x_blinding", t_xb[p]);
+        T[p].append_scalar("e_blinding", e_bl[p]);
+        wch[p] = T[p].challenge_scalar("w");
+        B.a.grow((size_t)Nl * sizeof(ScD) + 64);
+        B.b.grow((size_t)Nl * sizeof(ScD) + 64);
+        launch_lr_eval(as<ScD>(B.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(B.sL), as<ScD>(B.r0),
+                       as<ScD>(B.r1), as<ScD>(B.r3), as<ScD>(B.ypm), nl, Nl, mont(xx), mont(xx * xx), as<ScD>(B.a),
+                       as<ScD>(B.b), st);
     }
-    Scalar tb2 = from_dev(ws.small_host[1006]);   // <w_V, v_blinding>: every rank holds all of w_V
-    const Scalar tb1 = rb.tb[0], tb3 = rb.tb[1], tb4 = rb.tb[2], tb5 = rb.tb[3], tb6 = rb.tb[4];
-    uint8_t cT[5][32];
-    pedersen_commit(cT[0], tp[0], tb1);
-    pedersen_commit(cT[1], tp[2], tb3);
-    pedersen_commit(cT[2], tp[3], tb4);
-    pedersen_commit(cT[3], tp[4], tb5);
-    pedersen_commit(cT[4], tp[5], tb6);
-    T.append_point("T_1", cT[0]);
-    T.append_point("T_3", cT[1]);
-    T.append_point("T_4", cT[2]);
-    T.append_point("T_5", cT[3]);
-    T.append_point("T_6", cT[4]);
-    Scalar u = T.challenge_scalar("u"), x = T.challenge_scalar("x");
-    auto eval6 = [&](const Scalar c[6]) {
-        Scalar acc = x * c[5];
-        for (int k = 4; k >= 0; k--) acc = x * (c[k] + acc);
-        return acc;
-    };
-    Scalar tbs[6] = {tb1, tb2, tb3, tb4, tb5, tb6};
-    Scalar t_x = eval6(tp), t_xb = eval6(tbs);
-    Scalar e_bl = x * (i_bl + x * (o_bl + x * s_bl));
-    T.append_scalar("t_x", t_x);
-    T.append_scalar("t_x_blinding", t_xb);
-    T.append_scalar("e_blinding", e_bl);
-    Scalar wch = T.challenge_scalar("w");
-    Point Qp; mul_B(Qp, wch);
-    // Q in both base formats: cached for jobs over folded generators, affine
-    // Niels (Q, then -Q) for jobs over the level-0 generators
-    ws.Q.grow(sizeof(PtD) + 2 * sizeof(NielsD));
-    {
-        uint8_t qb[sizeof(PtD) + 2 * sizeof(NielsD)];
-        Point Qneg; pt_neg(Qneg, Qp);
-        pt_to_dev_cached(reinterpret_cast<uint32_t *>(qb), Qp);
-        pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD)), Qp);
-        pt_to_dev_niels(reinterpret_cast<uint32_t *>(qb + sizeof(PtD) + sizeof(NielsD)), Qneg);
-        memcpy(ws.small_host + 3000, qb, sizeof(qb));
-        BPG_HIP(hipMemcpyAsync(ws.Q.p, ws.small_host + 3000, sizeof(qb), hipMemcpyHostToDevice, st));
-    }
-    const PtD *Qc = as<PtD>(ws.Q);
-    const NielsD *Qn = reinterpret_cast<const NielsD *>(as<uint8_t>(ws.Q) + sizeof(PtD));
-    ws.a.grow((size_t)Nl * sizeof(ScD) + 64);
-    ws.b.grow((size_t)Nl * sizeof(ScD) + 64);
-    launch_lr_eval(as<ScD>(ws.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(ws.sL), as<ScD>(ws.r0), as<ScD>(ws.r1),
-                   as<ScD>(ws.r3), as<ScD>(ws.ypm), nl, Nl, mont(x), mont(x * x), as<ScD>(ws.a), as<ScD>(ws.b), st);
     double t2 = now_ms();
 
     // InnerProductProof::create with weighted single-scalar point folding
@@ -1072,16 +1090,23 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     // h / world). With comb tables (Nl >= 8) rounds 0 and 1 leave the level-1
     // generators unmaterialised: round 1's MSM expands them into level-0
     // generators and level 2 is built in one table pass.
-    T.append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
-    T.append_u64("n", N);
+    for (int p = 0; p < P; p++) {
+        T[p].append_message("dom-sep", (const uint8_t *)"ipp v1", 6);
+        T[p].append_u64("n", N);
+    }
     std::shared_ptr<CombTables> comb = cs.strat.tables() ? ctx.comb(gs, Nl) : nullptr;
-    std::vector<uint8_t> LRc(64 * (size_t)lgN);
-    Scalar lam = Scalar::one(), mu = Scalar::one();
-    const void *Gh = gs->G, *Hh = gs->H;
+    std::vector<std::vector<uint8_t>> LRc(P, std::vector<uint8_t>(64 * (size_t)lgN));
+    std::vector<Scalar> lam(P, Scalar::one()), mu(P, Scalar::one());
+    std::vector<const void *> Gh(P, gs->G), Hh(P, gs->H);
     int gfmt = MSM_NIELS;
-    ws.mscal.grow((size_t)(2 * Nl + 2) * sizeof(ScD) + 64);
-    if (Nl >= 2) {
-        for (int k = 0; k < 2; k++) { ws.Gp[k].grow((size_t)(Nl / 2) * sizeof(PtD)); ws.Hp[k].grow((size_t)(Nl / 2) * sizeof(PtD)); }
+    for (int p = 0; p < P; p++) {
+        ProofBufs &B = ws.pb[p];
+        B.mscal.grow((size_t)(2 * Nl + 2) * sizeof(ScD) + 64);
+        if (Nl >= 2)
+            for (int k = 0; k < 2; k++) {
+                B.Gp[k].grow((size_t)(Nl / 2) * sizeof(PtD));
+                B.Hp[k].grow((size_t)(Nl / 2) * sizeof(PtD));
+            }
     }
     // Round groups: after round k the fold is left pending (Ghat stays at
     // level k); round k+d's MSM expands each level-(k+d) base into its 2^d
@@ -1089,17 +1114,17 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
     // next level from level k: comb tables from the level-0 generators (a
     // pair), else the three- (pair) or seven-scalar (triple) Straus fold.
     const int group_cfg = cs.strat.group();
-    Scalar rho_h[2][4];   // the pending rounds' fold scalars (G a/b, H a/b), oldest first
+    std::vector<std::array<std::array<Scalar, 4>, 2>> rho_h(P);   // pending rounds' fold scalars, oldest first
     int depth = 0;        // pending levels: Ghat at level k, this round at level k + depth
-    int cur = -1;      // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
+    int cur = -1;         // buffer holding Ghat/Hhat: -1 the generators, else Gp/Hp[cur]
     // Tail (DESIGN.md "IPP tail without folds"): once a materialised level is
     // short, the remaining rounds keep it and weight its points instead of
     // folding them (each fold there is a latency-bound launch). The sharded
     // prover always ends in the tail: its last local round's fold is needed
-    // (as weights) for the final generator of each rank.
-    // sharded: the materialised levels are Nl/8^j (or /4^j, /2^j) after the
-    // first group, so the last one of at least 2 lanes has at most 8: a
-    // threshold of 8 or more always meets it
+    // (as weights) for the final generator of each rank. Sharded, the
+    // materialised levels are Nl/8^j (or /4^j, /2^j) after the first group,
+    // so the last one of at least 2 lanes has at most 8 lanes: a threshold
+    // of 8 or more always meets it.
     const uint32_t tail_len = sharded ? std::max<uint32_t>(cs.strat.tail(), 8u) : cs.strat.tail();
     bool tail = false;
     uint32_t M = 0;
@@ -1113,119 +1138,145 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
         if (!tail && depth == 0 && cur >= 0 && len <= tail_len && len >= (sharded ? 2u : 4u)) {
             tail = true;
             M = len;
-            ws.wG.grow((size_t)M * sizeof(ScD) + 64);
-            ws.wH.grow((size_t)M * sizeof(ScD) + 64);
-            launch_fill_scalars(as<ScD>(ws.wG), mont(Scalar::one()), M, st);
-            launch_fill_scalars(as<ScD>(ws.wH), mont(Scalar::one()), M, st);
+            for (int p = 0; p < P; p++) {
+                ProofBufs &B = ws.pb[p];
+                B.wG.grow((size_t)M * sizeof(ScD) + 64);
+                B.wH.grow((size_t)M * sizeof(ScD) + 64);
+                launch_fill_scalars(as<ScD>(B.wG), mont(Scalar::one()), M, st);
+                launch_fill_scalars(as<ScD>(B.wH), mont(Scalar::one()), M, st);
+            }
         }
-        IppRoundArgs A;
-        A.h = h; A.n = nl;
-        A.lamG1 = mont(lam); A.lamGu = mont(lam * u);
-        A.muH1 = mont(mu); A.muHu = mont(mu * u);
-        ScD *ms = as<ScD>(ws.mscal);
         // MSM bases: the level-0 generators (affine Niels), else Ghat/Hhat (cached)
         const int mfmt = cur < 0 ? MSM_NIELS : MSM_CACHED;
-        const void *Gm = cur < 0 ? G0 : Gh, *Hm = cur < 0 ? H0 : Hh;
-        const void *Qb = mfmt == MSM_NIELS ? (const void *)Qn : (const void *)Qc;
         const size_t ps = mfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
-        // Niels jobs gather negated level-0 generators / -Q for negative digits
-        const int64_t gn = mfmt == MSM_NIELS ? gneg : 0, qn = mfmt == MSM_NIELS ? 1 : 0;
-        MsmSeg seg[MSM_MAX_SEGS];
+        // Niels jobs gather negated level-0 generators for negative digits
+        const int64_t gn = mfmt == MSM_NIELS ? gneg : 0;
         auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
-        int nseg;
         const bool lazy = depth == 1;
         const size_t hh = h;
-        if (tail) {
-            launch_ipp_prep_tail(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, M, as<ScD>(ws.wG),
-                                 as<ScD>(ws.wH), ms, as<ScD>(ws.partial), st);
-            const size_t mm_ = M;
-            MsmSeg sl[6] = {{ms, Gh, M, 0}, {ms + mm_, Hh, M, 0}, {ms + 4 * mm_, Qb, 1, 0},
-                            {ms + 2 * mm_, Gh, M, 1}, {ms + 3 * mm_, Hh, M, 1}, {ms + 4 * mm_ + 1, Qb, 1, 1}};
-            std::copy(sl, sl + 6, seg);
-            nseg = 6;
-        } else if (lazy) {
-            const uint32_t h0 = 2 * h;
-            LazyArgs Z;
-            Z.h0 = h0;
-            Z.rGa = mont(rho_h[0][0]); Z.rGb = mont(rho_h[0][1]); Z.rHa = mont(rho_h[0][2]); Z.rHb = mont(rho_h[0][3]);
-            launch_ipp_prep_lazy(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
-            MsmSeg sl[10] = {{ms, at(Gm, h), h, 0, gn}, {ms + hh, at(Gm, h + h0), h, 0, gn}, {ms + 2 * hh, Hm, h, 0, gn},
-                             {ms + 3 * hh, at(Hm, h0), h, 0, gn}, {ms + 8 * hh, Qb, 1, 0, qn},
-                             {ms + 4 * hh, Gm, h, 1, gn}, {ms + 5 * hh, at(Gm, h0), h, 1, gn},
-                             {ms + 6 * hh, at(Hm, h), h, 1, gn}, {ms + 7 * hh, at(Hm, h + h0), h, 1, gn},
-                             {ms + 8 * hh + 1, Qb, 1, 1, qn}};
-            std::copy(sl, sl + 10, seg);
-            nseg = 10;
-        } else if (depth == 2) {
-            // bases at level k+2 expanded into level k: family f, term t at
-            // out[(4f + t) h], point offset x0(f) + 2h t
-            Deep2Args Z;
-            for (int v = 0; v < 2; v++)
-                for (int c = 0; c < 2; c++) { Z.r0[v][c] = mont(rho_h[0][2 * v + c]); Z.r1[v][c] = mont(rho_h[1][2 * v + c]); }
-            launch_ipp_prep_deep2(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, Z, ms, as<ScD>(ws.partial), st);
-            nseg = 0;
-            for (int f = 0; f < 4; f++) {
-                const void *B = (f & 1) ? Hm : Gm;
-                const size_t x0 = (f == 0 || f == 3) ? hh : 0;
-                for (int t = 0; t < 4; t++)
-                    seg[nseg++] = {ms + (size_t)(4 * f + t) * hh, at(B, x0 + 2 * hh * t), h, (uint32_t)(f >> 1), gn};
-                if (f == 1) seg[nseg++] = {ms + 16 * hh, Qb, 1, 0, qn};
+        MsmSeg seg[MSM_MAX_SEGS];
+        int nseg = 0;
+        size_t cofs = 0;   // c_L, c_R at mscal[cofs], [cofs + 1]
+        for (int p = 0; p < P; p++) {
+            ProofBufs &B = ws.pb[p];
+            IppRoundArgs A;
+            A.h = h; A.n = nl;
+            A.lamG1 = mont(lam[p]); A.lamGu = mont(lam[p] * u[p]);
+            A.muH1 = mont(mu[p]); A.muHu = mont(mu[p] * u[p]);
+            ScD *ms = as<ScD>(B.mscal);
+            const void *Gm = cur < 0 ? G0 : Gh[p], *Hm = cur < 0 ? H0 : Hh[p];
+            const uint32_t L0 = 2 * (uint32_t)p, R0 = L0 + 1;   // this proof's L and R MSMs
+            if (tail) {
+                launch_ipp_prep_tail(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, M, as<ScD>(B.wG),
+                                     as<ScD>(B.wH), ms, as<ScD>(B.partial), st);
+                const size_t mm_ = M;
+                seg[nseg++] = {ms, Gh[p], M, L0};
+                seg[nseg++] = {ms + mm_, Hh[p], M, L0};
+                seg[nseg++] = {ms + 2 * mm_, Gh[p], M, R0};
+                seg[nseg++] = {ms + 3 * mm_, Hh[p], M, R0};
+                cofs = 4 * mm_;
+            } else if (lazy) {
+                const uint32_t h0 = 2 * h;
+                LazyArgs Z;
+                Z.h0 = h0;
+                Z.rGa = mont(rho_h[p][0][0]); Z.rGb = mont(rho_h[p][0][1]);
+                Z.rHa = mont(rho_h[p][0][2]); Z.rHb = mont(rho_h[p][0][3]);
+                launch_ipp_prep_lazy(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), st);
+                seg[nseg++] = {ms, at(Gm, h), h, L0, gn};
+                seg[nseg++] = {ms + hh, at(Gm, h + h0), h, L0, gn};
+                seg[nseg++] = {ms + 2 * hh, Hm, h, L0, gn};
+                seg[nseg++] = {ms + 3 * hh, at(Hm, h0), h, L0, gn};
+                seg[nseg++] = {ms + 4 * hh, Gm, h, R0, gn};
+                seg[nseg++] = {ms + 5 * hh, at(Gm, h0), h, R0, gn};
+                seg[nseg++] = {ms + 6 * hh, at(Hm, h), h, R0, gn};
+                seg[nseg++] = {ms + 7 * hh, at(Hm, h + h0), h, R0, gn};
+                cofs = 8 * hh;
+            } else if (depth == 2) {
+                // bases at level k+2 expanded into level k: family f, term t at
+                // out[(4f + t) h], point offset x0(f) + 2h t
+                Deep2Args Z;
+                for (int v = 0; v < 2; v++)
+                    for (int c = 0; c < 2; c++) {
+                        Z.r0[v][c] = mont(rho_h[p][0][2 * v + c]);
+                        Z.r1[v][c] = mont(rho_h[p][1][2 * v + c]);
+                    }
+                launch_ipp_prep_deep2(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), st);
+                for (int f = 0; f < 4; f++) {
+                    const void *Bs = (f & 1) ? Hm : Gm;
+                    const size_t x0 = (f == 0 || f == 3) ? hh : 0;
+                    for (int t = 0; t < 4; t++)
+                        seg[nseg++] = {ms + (size_t)(4 * f + t) * hh, at(Bs, x0 + 2 * hh * t), h,
+                                       (uint32_t)(f >> 1) + L0, gn};
+                }
+                cofs = 16 * hh;
+            } else {
+                launch_ipp_prep(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, ms, as<ScD>(B.partial), st);
+                // points whose a-scalar is zero (padding lanes) are left out of
+                // the job: L's G part runs over a_lo, R's over a_hi
+                const uint32_t nLG = std::min(h, anz), nRG = anz > h ? std::min(h, anz - h) : 0u;
+                const MsmSeg sl[4] = {{ms, at(Gm, h), nLG, L0, gn}, {ms + hh, Hm, h, L0, gn},
+                                      {ms + 2 * hh, Gm, nRG, R0, gn}, {ms + 3 * hh, at(Hm, h), h, R0, gn}};
+                for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
+                cofs = 4 * hh;
             }
-            seg[nseg++] = {ms + 16 * hh + 1, Qb, 1, 1, qn};
-        } else {
-            launch_ipp_prep(as<ScD>(ws.a), as<ScD>(ws.b), as<ScD>(ws.yipm), A, ms, as<ScD>(ws.partial), st);
-            // points whose a-scalar is zero (padding lanes) are left out of
-            // the job: L's G part runs over a_lo, R's over a_hi
-            const uint32_t nLG = std::min(h, anz), nRG = anz > h ? std::min(h, anz - h) : 0u;
-            MsmSeg sl[6] = {{ms, at(Gm, h), nLG, 0, gn}, {ms + hh, Hm, h, 0, gn}, {ms + 4 * hh, Qb, 1, 0, qn},
-                            {ms + 2 * hh, Gm, nRG, 1, gn}, {ms + 3 * hh, at(Hm, h), h, 1, gn},
-                            {ms + 4 * hh + 1, Qb, 1, 1, qn}};
-            nseg = 0;
-            for (const MsmSeg &x : sl) if (x.count) seg[nseg++] = x;
+            BPG_HIP(hipMemcpyAsync(B.small_host + 1020, ms + cofs, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
         }
-        int ph = ws.prof_begin("msm_ipp", ((tail ? 2.0 * M : (4.0 * h) * (1 << depth)) + 2) * (64 + 32));
-        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2, rowsLR, mfmt);
+        int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));
+        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt);
         ws.prof_end(ph);
         ws.sync();
-        Point LR[2];
-        combine_rows(LR[0], rowsLR, pl.W, pl.c);
-        combine_rows(LR[1], rowsLR + pl.W, pl.W, pl.c);
-        if (sharded) {   // c_L Q and c_R Q are inside the partials: sum L and R
-            std::vector<Point> sum = allgather_point_sums(*ag, LR, 2, world);
-            LR[0] = sum[0]; LR[1] = sum[1];
+        std::vector<std::array<Scalar, 4>> rnow(P);   // this round's fold scalars (G a/b, H a/b)
+        for (int p = 0; p < P; p++) {
+            ProofBufs &B = ws.pb[p];
+            Point LR[2], cq;
+            combine_rows(LR[0], rowsLR + (2 * p) * pl.W, pl.W, pl.c);
+            combine_rows(LR[1], rowsLR + (2 * p + 1) * pl.W, pl.W, pl.c);
+            // + c_L Q, + c_R Q (this rank's share of c_L, c_R when sharded)
+            for (int s = 0; s < 2; s++) {
+                mul_B(cq, from_dev(B.small_host[1020 + s]) * wch[p]);
+                pt_add(LR[s], LR[s], cq);
+            }
+            if (sharded) {   // sum the ranks' partial L and R
+                std::vector<Point> sum = allgather_point_sums(*ag, LR, 2, world);
+                LR[0] = sum[0]; LR[1] = sum[1];
+            }
+            uint8_t *cl = LRc[p].data() + 64 * (size_t)k, *cr = cl + 32;
+            ristretto_compress(cl, LR[0]);
+            ristretto_compress(cr, LR[1]);
+            T[p].append_point("L", cl);
+            T[p].append_point("R", cr);
+            const Scalar uk = T[p].challenge_scalar("u");
+            const Scalar uinv = sc_invert(uk);
+            launch_ipp_fold_scalars(as<ScD>(B.a), as<ScD>(B.b), h, mont(uk), mont(uinv), st);
+            const Scalar u2 = uk * uk, ui2 = uinv * uinv;
+            const Scalar yh = sc_pow_u64(y_inv[p], (uint64_t)h * world);   // the round's global half length
+            rnow[p] = {u2, u2 * u[p], ui2 * yh, ui2 * yh * u[p]};
+            lam[p] = lam[p] * uinv;
+            mu[p] = mu[p] * uk;
         }
-        uint8_t *cl = LRc.data() + 64 * (size_t)k, *cr = cl + 32;
-        ristretto_compress(cl, LR[0]);
-        ristretto_compress(cr, LR[1]);
-        T.append_point("L", cl);
-        T.append_point("R", cr);
-        Scalar uk = T.challenge_scalar("u");
-        Scalar uinv = sc_invert(uk);
-        launch_ipp_fold_scalars(as<ScD>(ws.a), as<ScD>(ws.b), h, mont(uk), mont(uinv), st);
-        Scalar u2 = uk * uk, ui2 = uinv * uinv;
-        Scalar yh = sc_pow_u64(y_inv, (uint64_t)h * world);   // the round's global half length
-        Scalar rGa = u2, rGb = u2 * u, rHa = ui2 * yh, rHb = rHa * u;
         const int nxt = cur == 0 ? 1 : 0;
         if (tail) {
             if (h > 1 || sharded)
-                launch_ipp_tail_weights(as<ScD>(ws.wG), as<ScD>(ws.wH), M, h, nl, mont(rGa), mont(rGb), mont(rHa),
-                                        mont(rHb), st);
+                for (int p = 0; p < P; p++)
+                    launch_ipp_tail_weights(as<ScD>(ws.pb[p].wG), as<ScD>(ws.pb[p].wH), M, h, nl, mont(rnow[p][0]),
+                                            mont(rnow[p][1]), mont(rnow[p][2]), mont(rnow[p][3]), st);
         } else if (h > 1) {
             const int group = (comb && cur < 0) ? 2 : group_cfg;
-            const Scalar rnow[4] = {rGa, rGb, rHa, rHb};
             if (depth + 1 < group) {   // level k + depth + 1 stays implicit
-                std::copy(rnow, rnow + 4, rho_h[depth]);
+                for (int p = 0; p < P; p++) rho_h[p][depth] = rnow[p];
                 depth++;
             } else if (depth == 0) {
-                PtD *Gn = as<PtD>(ws.Gp[nxt]), *Hn = as<PtD>(ws.Hp[nxt]);
-                launch_ipp_fold_points(Gh, Hh, gfmt, h, nl, to_dev(rGa), to_dev(rGb), to_dev(rHa), to_dev(rHb), Gn, Hn,
-                                       ws.fold_stage, st);
-                Gh = Gn; Hh = Hn;
+                for (int p = 0; p < P; p++) {
+                    ProofBufs &B = ws.pb[p];
+                    PtD *Gn = as<PtD>(B.Gp[nxt]), *Hn = as<PtD>(B.Hp[nxt]);
+                    launch_ipp_fold_points(Gh[p], Hh[p], gfmt, h, nl, to_dev(rnow[p][0]), to_dev(rnow[p][1]),
+                                           to_dev(rnow[p][2]), to_dev(rnow[p][3]), Gn, Hn, B.fold_stage, st);
+                    Gh[p] = Gn; Hh[p] = Hn;
+                }
                 cur = nxt;
                 gfmt = MSM_CACHED;
             } else if (depth == 1) {
                 // level k+2 from level k: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
-                const Scalar *rho_p = rho_h[0];
                 const uint32_t h1 = h, h0 = 2 * h;
                 std::vector<int64_t> cut = {0, (int64_t)h1, (int64_t)nl - h1, (int64_t)nl, (int64_t)nl - h0,
                                             (int64_t)nl - h0 - h1};
@@ -1233,41 +1284,45 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 for (int64_t c : cut) if (c >= 0 && c < (int64_t)h1) starts.push_back((uint32_t)c);
                 std::sort(starts.begin(), starts.end());
                 starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
-                ScD coef[2][COMB_MAXRANGE][3];
                 const bool table = comb && cur < 0;
-                CombArgs C{};
-                C.nrange = (uint32_t)starts.size();
-                for (uint32_t r = 0; r < C.nrange; r++) {
-                    const uint64_t i = starts[r];
-                    C.rstart[r] = (uint32_t)i;
-                    const bool b1 = i < nl && i + h1 >= nl, b0 = i < nl && i + h0 >= nl,
-                               b0h = i + h1 < nl && i + h1 + h0 >= nl;
-                    for (int v = 0; v < 2; v++) {
-                        const Scalar c1 = rnow[2 * v + (b1 ? 1 : 0)];
-                        const Scalar c2 = rho_p[2 * v + (b0 ? 1 : 0)];
-                        const Scalar c3 = c1 * rho_p[2 * v + (b0h ? 1 : 0)];
-                        if (table) {
-                            uint8_t sb[3][32];
-                            c1.reduced().to_bytes(sb[0]); c2.reduced().to_bytes(sb[1]); c3.reduced().to_bytes(sb[2]);
-                            comb_digits(sb[0], C.dig[v][r][0]);
-                            comb_digits(sb[1], C.dig[v][r][1]);
-                            comb_digits(sb[2], C.dig[v][r][2]);
-                        } else {
-                            coef[v][r][0] = to_dev(c1); coef[v][r][1] = to_dev(c2); coef[v][r][2] = to_dev(c3);
+                for (int p = 0; p < P; p++) {
+                    ProofBufs &B = ws.pb[p];
+                    const std::array<Scalar, 4> &rho_p = rho_h[p][0];
+                    ScD coef[2][COMB_MAXRANGE][3];
+                    CombArgs C{};
+                    C.nrange = (uint32_t)starts.size();
+                    for (uint32_t r = 0; r < C.nrange; r++) {
+                        const uint64_t i = starts[r];
+                        C.rstart[r] = (uint32_t)i;
+                        const bool b1 = i < nl && i + h1 >= nl, b0 = i < nl && i + h0 >= nl,
+                                   b0h = i + h1 < nl && i + h1 + h0 >= nl;
+                        for (int v = 0; v < 2; v++) {
+                            const Scalar c1 = rnow[p][2 * v + (b1 ? 1 : 0)];
+                            const Scalar c2 = rho_p[2 * v + (b0 ? 1 : 0)];
+                            const Scalar c3 = c1 * rho_p[2 * v + (b0h ? 1 : 0)];
+                            if (table) {
+                                uint8_t sb[3][32];
+                                c1.reduced().to_bytes(sb[0]); c2.reduced().to_bytes(sb[1]); c3.reduced().to_bytes(sb[2]);
+                                comb_digits(sb[0], C.dig[v][r][0]);
+                                comb_digits(sb[1], C.dig[v][r][1]);
+                                comb_digits(sb[2], C.dig[v][r][2]);
+                            } else {
+                                coef[v][r][0] = to_dev(c1); coef[v][r][1] = to_dev(c2); coef[v][r][2] = to_dev(c3);
+                            }
                         }
                     }
+                    if (table) {
+                        C.gens[0] = gs->G; C.gens[1] = gs->H;
+                        C.tab[0] = comb->tabG; C.tab[1] = comb->tabH;
+                        C.out[0] = B.Gp[nxt].p; C.out[1] = B.Hp[nxt].p;
+                        C.h1 = h1; C.ntab = 3 * h1;
+                        launch_ipp_comb_fold(C, B.comb_stage, st);
+                    } else {
+                        launch_ipp_fold2(Gh[p], Hh[p], gfmt, h1, C.nrange, C.rstart, coef, as<PtD>(B.Gp[nxt]),
+                                         as<PtD>(B.Hp[nxt]), B.fold2_stage, st);
+                    }
+                    Gh[p] = B.Gp[nxt].p; Hh[p] = B.Hp[nxt].p;
                 }
-                if (table) {
-                    C.gens[0] = gs->G; C.gens[1] = gs->H;
-                    C.tab[0] = comb->tabG; C.tab[1] = comb->tabH;
-                    C.out[0] = ws.Gp[nxt].p; C.out[1] = ws.Hp[nxt].p;
-                    C.h1 = h1; C.ntab = 3 * h1;
-                    launch_ipp_comb_fold(C, ws.comb_stage, st);
-                } else {
-                    launch_ipp_fold2(Gh, Hh, gfmt, h1, C.nrange, C.rstart, coef, as<PtD>(ws.Gp[nxt]),
-                                     as<PtD>(ws.Hp[nxt]), ws.fold2_stage, st);
-                }
-                Gh = ws.Gp[nxt].p; Hh = ws.Hp[nxt].p;
                 cur = nxt;
                 gfmt = MSM_CACHED;
                 depth = 0;
@@ -1277,7 +1332,6 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 // k+1 (lane i + b2 hq) and round k (lane i + b2 hq + 2 b1 hq);
                 // each set bit contributes its round's scalar for that lane's class
                 const uint32_t hq = h;
-                const Scalar *rr[3] = {rho_h[0], rho_h[1], rnow};
                 std::vector<uint32_t> starts = {0};
                 for (int j = 0; j <= 8; j++) {
                     const int64_t c = (int64_t)nl - (int64_t)j * hq;
@@ -1286,82 +1340,94 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 std::sort(starts.begin(), starts.end());
                 starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
                 if (starts.size() > COMB_MAXRANGE) throw std::runtime_error("fold3 ranges");
-                ScD coef[2][COMB_MAXRANGE][7];
-                auto cls = [&](uint64_t x, uint64_t half) { return x < nl && x + half >= nl ? 1 : 0; };
-                for (size_t r = 0; r < starts.size(); r++) {
-                    const uint64_t i = starts[r];
-                    for (int t = 1; t < 8; t++) {
-                        const int b0 = (t >> 2) & 1, b1 = (t >> 1) & 1, b2 = t & 1;
-                        const uint64_t x2 = i, x1 = i + (uint64_t)b2 * hq, x0 = x1 + (uint64_t)b1 * 2 * hq;
-                        for (int v = 0; v < 2; v++) {
-                            Scalar c = Scalar::one();
-                            if (b2) c = c * rr[2][2 * v + cls(x2, hq)];
-                            if (b1) c = c * rr[1][2 * v + cls(x1, 2 * (uint64_t)hq)];
-                            if (b0) c = c * rr[0][2 * v + cls(x0, 4 * (uint64_t)hq)];
-                            coef[v][r][t - 1] = to_dev(c);
+                auto cls = [&](uint64_t xx, uint64_t half) { return xx < nl && xx + half >= nl ? 1 : 0; };
+                for (int p = 0; p < P; p++) {
+                    ProofBufs &B = ws.pb[p];
+                    const std::array<Scalar, 4> *rr[3] = {&rho_h[p][0], &rho_h[p][1], &rnow[p]};
+                    ScD coef[2][COMB_MAXRANGE][7];
+                    for (size_t r = 0; r < starts.size(); r++) {
+                        const uint64_t i = starts[r];
+                        for (int t = 1; t < 8; t++) {
+                            const int b0 = (t >> 2) & 1, b1 = (t >> 1) & 1, b2 = t & 1;
+                            const uint64_t x2 = i, x1 = i + (uint64_t)b2 * hq, x0 = x1 + (uint64_t)b1 * 2 * hq;
+                            for (int v = 0; v < 2; v++) {
+                                Scalar c = Scalar::one();
+                                if (b2) c = c * (*rr[2])[2 * v + cls(x2, hq)];
+                                if (b1) c = c * (*rr[1])[2 * v + cls(x1, 2 * (uint64_t)hq)];
+                                if (b0) c = c * (*rr[0])[2 * v + cls(x0, 4 * (uint64_t)hq)];
+                                coef[v][r][t - 1] = to_dev(c);
+                            }
                         }
                     }
+                    const size_t tb = ipp_fold3_table_bytes(hq, (uint32_t)starts.size());
+                    B.f3tab.grow(tb);
+                    launch_ipp_fold3(Gh[p], Hh[p], gfmt, hq, (uint32_t)starts.size(), starts.data(), coef,
+                                     as<PtD>(B.Gp[nxt]), as<PtD>(B.Hp[nxt]), B.f3tab.p, B.f3tab.cap, B.fold3_stage, st);
+                    Gh[p] = B.Gp[nxt].p; Hh[p] = B.Hp[nxt].p;
                 }
-                const size_t tb = ipp_fold3_table_bytes(hq, (uint32_t)starts.size());
-                ws.f3tab.grow(tb);
-                launch_ipp_fold3(Gh, Hh, gfmt, hq, (uint32_t)starts.size(), starts.data(), coef, as<PtD>(ws.Gp[nxt]),
-                                 as<PtD>(ws.Hp[nxt]), ws.f3tab.p, ws.f3tab.cap, ws.fold3_stage, st);
-                Gh = ws.Gp[nxt].p; Hh = ws.Hp[nxt].p;
                 cur = nxt;
                 gfmt = MSM_CACHED;
                 depth = 0;
             }
         }
-        lam = lam * uinv;
-        mu = mu * uk;
         len = h;
         anz = std::min(anz, h);
     }
-    BPG_HIP(hipMemcpyAsync(ws.small_host + 1010, ws.a.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
-    BPG_HIP(hipMemcpyAsync(ws.small_host + 1011, ws.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    for (int p = 0; p < P; p++) {
+        ProofBufs &B = ws.pb[p];
+        BPG_HIP(hipMemcpyAsync(B.small_host + 1010, B.a.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
+        BPG_HIP(hipMemcpyAsync(B.small_host + 1011, B.b.p, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    }
     Point Gfin, Hfin;   // sharded: this rank's last generator pair (weighted sum of the tail level)
     if (sharded) {
         if (!tail) throw std::runtime_error("sharded prove ended outside the IPP tail");
-        ws.wconv.grow(2 * (size_t)M * sizeof(ScD) + 64);
-        ScD *wc = as<ScD>(ws.wconv);
-        launch_from_mont(as<ScD>(ws.wG), M, wc, st);
-        launch_from_mont(as<ScD>(ws.wH), M, wc + M, st);
-        MsmSeg sl[2] = {{wc, Gh, M, 0}, {wc + M, Hh, M, 1}};
+        ProofBufs &B = ws.pb[0];
+        B.wconv.grow(2 * (size_t)M * sizeof(ScD) + 64);
+        ScD *wc = as<ScD>(B.wconv);
+        launch_from_mont(as<ScD>(B.wG), M, wc, st);
+        launch_from_mont(as<ScD>(B.wH), M, wc + M, st);
+        MsmSeg sl[2] = {{wc, Gh[0], M, 0}, {wc + M, Hh[0], M, 1}};
         MsmPlan pl = ws.msm->enqueue(sl, 2, 2, rowsLR, MSM_CACHED);
         ws.sync();
         combine_rows(Gfin, rowsLR, pl.W, pl.c);
         combine_rows(Hfin, rowsLR + pl.W, pl.W, pl.c);
     }
     ws.sync();
-    Scalar fa = from_dev(ws.small_host[1010]), fb = from_dev(ws.small_host[1011]);
+    std::vector<Scalar> fa(P), fb(P);
+    for (int p = 0; p < P; p++) {
+        fa[p] = from_dev(ws.pb[p].small_host[1010]);
+        fb[p] = from_dev(ws.pb[p].small_host[1011]);
+    }
     if (sharded) {
         // the last lg(world) rounds over one lane per rank (global lane i =
         // rank), dalek's InnerProductProof::create on the host: true
         // generators G_i = lam * Gf_i * Ghat_i, H_i = mu * y^-i * Gf_i * Hhat_i
-        const Scalar gf = rank < n ? Scalar::one() : u;
+        const Scalar gf = rank < n ? Scalar::one() : u[0];
         Point t;
-        mul_var(t, lam * gf, Gfin); Gfin = t;
-        mul_var(t, mu * sc_pow_u64(y_inv, rank) * gf, Hfin); Hfin = t;
+        mul_var(t, lam[0] * gf, Gfin); Gfin = t;
+        mul_var(t, mu[0] * sc_pow_u64(y_inv[0], rank) * gf, Hfin); Hfin = t;
         std::vector<uint8_t> send(128), recv(128 * (size_t)world);
-        fa.to_bytes(send.data()); fb.to_bytes(send.data() + 32);
+        fa[0].to_bytes(send.data()); fb[0].to_bytes(send.data() + 32);
         ristretto_compress(send.data() + 64, Gfin);
         ristretto_compress(send.data() + 96, Hfin);
         (*ag)(send.data(), send.size(), recv.data());
         std::vector<Scalar> va(world), vb(world);
         std::vector<Point> vG(world), vH(world);
         for (uint32_t r = 0; r < world; r++) {
-            const uint8_t *p = recv.data() + 128 * (size_t)r;
-            va[r] = Scalar::reduce(p);
-            vb[r] = Scalar::reduce(p + 32);
-            if (!ristretto_decompress(vG[r], p + 64) || !ristretto_decompress(vH[r], p + 96))
+            const uint8_t *q = recv.data() + 128 * (size_t)r;
+            va[r] = Scalar::reduce(q);
+            vb[r] = Scalar::reduce(q + 32);
+            if (!ristretto_decompress(vG[r], q + 64) || !ristretto_decompress(vH[r], q + 96))
                 throw std::runtime_error("sharded prove: a rank sent an invalid generator");
         }
+        Point Qp;
+        mul_B(Qp, wch[0]);
         for (uint32_t L = world; L > 1; L /= 2, k++) {
             const uint32_t h = L / 2;
             Scalar cL = Scalar::zero(), cR = Scalar::zero();
             Point Lp, Rp;
             pt_identity(Lp); pt_identity(Rp);
-            auto madd = [&](Point &acc, const Scalar &s, const Point &p) { Point q, r; mul_var(q, s, p); pt_add(r, acc, q); acc = r; };
+            auto madd = [&](Point &acc, const Scalar &s, const Point &pt) { Point q, r; mul_var(q, s, pt); pt_add(r, acc, q); acc = r; };
             for (uint32_t i = 0; i < h; i++) {
                 cL = cL + va[i] * vb[h + i];
                 cR = cR + va[h + i] * vb[i];
@@ -1369,12 +1435,12 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 madd(Rp, va[h + i], vG[i]); madd(Rp, vb[i], vH[h + i]);
             }
             madd(Lp, cL, Qp); madd(Rp, cR, Qp);
-            uint8_t *cl = LRc.data() + 64 * (size_t)k, *cr = cl + 32;
+            uint8_t *cl = LRc[0].data() + 64 * (size_t)k, *cr = cl + 32;
             ristretto_compress(cl, Lp);
             ristretto_compress(cr, Rp);
-            T.append_point("L", cl);
-            T.append_point("R", cr);
-            const Scalar uk = T.challenge_scalar("u"), uinv = sc_invert(uk);
+            T[0].append_point("L", cl);
+            T[0].append_point("R", cr);
+            const Scalar uk = T[0].challenge_scalar("u"), uinv = sc_invert(uk);
             for (uint32_t i = 0; i < h; i++) {
                 va[i] = va[i] * uk + va[h + i] * uinv;
                 vb[i] = vb[i] * uinv + vb[h + i] * uk;
@@ -1383,34 +1449,43 @@ std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, s
                 mul_var(h1, uk, vH[i]); mul_var(h2, uinv, vH[h + i]); pt_add(vH[i], h1, h2);
             }
         }
-        fa = va[0];
-        fb = vb[0];
+        fa[0] = va[0];
+        fb[0] = vb[0];
     }
     ws.prof_flush();
     double t3 = now_ms();
 
     // R1CSProof::to_bytes (one-phase)
-    std::vector<uint8_t> proof;
-    proof.reserve(417 + 64 * (size_t)lgN);
-    proof.push_back(0);
-    auto put = [&](const uint8_t *p) { proof.insert(proof.end(), p, p + 32); };
-    put(cAI); put(cAO); put(cS);
-    for (int i = 0; i < 5; i++) put(cT[i]);
-    uint8_t b32[32];
-    t_x.to_bytes(b32); put(b32);
-    t_xb.to_bytes(b32); put(b32);
-    e_bl.to_bytes(b32); put(b32);
-    proof.insert(proof.end(), LRc.begin(), LRc.end());
-    fa.to_bytes(b32); put(b32);
-    fb.to_bytes(b32); put(b32);
-    ProveTimings t;
-    t.commit_ms = t1 - t0;
-    t.vec_ms = t2 - t1;
-    t.ipp_ms = t3 - t2;
-    t.total_ms = t3 - t0;
-    last_timings() = t;
-    if (tm) *tm = t;
-    return proof;
+    std::vector<std::vector<uint8_t>> proofs(P);
+    for (int p = 0; p < P; p++) {
+        std::vector<uint8_t> &proof = proofs[p];
+        proof.reserve(417 + 64 * (size_t)lgN);
+        proof.push_back(0);
+        auto put = [&](const uint8_t *q) { proof.insert(proof.end(), q, q + 32); };
+        put(cA[p].data()); put(cA[p].data() + 32); put(cA[p].data() + 64);
+        for (int i = 0; i < 5; i++) put(cT[p].data() + 32 * i);
+        uint8_t b32[32];
+        t_x[p].to_bytes(b32); put(b32);
+        t_xb[p].to_bytes(b32); put(b32);
+        e_bl[p].to_bytes(b32); put(b32);
+        proof.insert(proof.end(), LRc[p].begin(), LRc[p].end());
+        fa[p].to_bytes(b32); put(b32);
+        fb[p].to_bytes(b32); put(b32);
+        ProveTimings t;
+        t.commit_ms = t1 - t0;
+        t.vec_ms = t2 - t1;
+        t.ipp_ms = t3 - t2;
+        t.total_ms = t3 - t0;
+        last_timings() = t;
+        if (tms) tms[p] = t;
+    }
+    return proofs;
+}
+
+std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
+                                   ProveTimings *tm, const AllGather *ag) {
+    const RngBlock *rbp = &rb;
+    return gpu_prove_lockstep(cs, label, label_len, &rbp, 1, tm, ag)[0];
 }
 
 // ------------------------------------------------------------------ verify
@@ -1481,14 +1556,9 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     // device: flattened_constraints(z), y^-i
     Scalar y_inv = sc_invert(y);
     ws.yipm.grow((size_t)N * sizeof(ScD));
-    {
-        DBuf lo2, hi2;
-        pow_vector(ws, 2, y_inv, N, lo2, hi2, as<ScD>(ws.yipm));
-        pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);
-        ws.sync();
-        if (lo2.p) (void)hipFree(lo2.p);
-        if (hi2.p) (void)hipFree(hi2.p);
-    }
+    pow_vector(ws, 2, y_inv, N, ws.ylo, ws.yhi, as<ScD>(ws.yipm));
+    pow_vector(ws, 4, z, cs.q + 2, ws.zlo, ws.zhi, nullptr);
+    ws.sync();
     ws.w.grow((size_t)cs.ncol * sizeof(ScD) + 64);
     CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
                as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),

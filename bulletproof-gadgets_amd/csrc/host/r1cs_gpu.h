@@ -159,6 +159,12 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
 // partial sums; all ranks return the same proof bytes.
 std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
                                    ProveTimings *tm = nullptr, const AllGather *ag = nullptr);
+// The same for P (<= 2) proofs of one circuit in lockstep on the calling
+// thread's stream (one MSM job per step for all of them); tms: P entries or
+// null. P must be 1 when sharded.
+std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
+                                                     const RngBlock *const *rbs, int P, ProveTimings *tms = nullptr,
+                                                     const AllGather *ag = nullptr);
 // Verifier::verify; returns 1 accept / 0 reject.
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                const uint8_t *proof, size_t proof_len, const uint8_t entropy[32]);
