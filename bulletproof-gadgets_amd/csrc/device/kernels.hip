@@ -215,6 +215,7 @@ struct SegTab {
 // gathers from a per-block pointer table in LDS without searching segments
 #define MSM_SEG_SHIFT 26
 #define MSM_LOC_MASK ((1u << MSM_SEG_SHIFT) - 1)
+static_assert(MSM_MAXSEG <= 32, "an entry's segment field is 5 bits");
 DEVI int seg_of(const SegTab &T, uint32_t g) {
     int si = 0;
 #pragma unroll

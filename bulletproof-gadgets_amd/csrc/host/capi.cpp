@@ -405,7 +405,11 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
             return v >= 2 ? 2 : 1;
         }();
         uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
-        std::vector<uint8_t *> slot = cs.slots(nslots, 2 * (size_t)cs.n * 64 + 64);
+        // BPG_HOST_SLOTS=1: producers write the draws into pinned host slots
+        // and each consumer copies its proof's draws up on its own stream, so
+        // the producers need no HIP streams (and hardware queues) at all
+        static const bool host_slots = [] { const char *e = getenv("BPG_HOST_SLOTS"); return e && e[0] == '1'; }();
+        std::vector<uint8_t *> slot = cs.slots(nslots, 2 * (size_t)cs.n * 64 + 64, host_slots);
         std::mutex mu;
         std::condition_variable cv;
         std::vector<int> free_slots;
@@ -445,10 +449,10 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                         for (uint32_t i = 0; i < cnt; i++) {
                             ent[i] = entropy + 32 * (size_t)(k0 + i);
                             blocks[k0 + i].wide = slot[slot_of[k0 + i]];
-                            blocks[k0 + i].on_device = true;
+                            blocks[k0 + i].on_device = !host_slots;
                             out[i] = &blocks[k0 + i];
                         }
-                        rng_draw_group(cs, label, label_len, ent, (int)cnt, out, true);
+                        rng_draw_group(cs, label, label_len, ent, (int)cnt, out, !host_slots);
                         std::lock_guard<std::mutex> lk(mu);
                         for (uint32_t i = 0; i < cnt; i++) ready.push_back(k0 + i);
                         cv.notify_all();

@@ -434,24 +434,28 @@ template <class T>
 static T *as(DBuf &b) { return reinterpret_cast<T *>(b.p); }
 
 // ------------------------------------------------------------------ prepare
-std::vector<uint8_t *> PreparedCS::slots(size_t count, size_t bytes) const {
+std::vector<uint8_t *> PreparedCS::slots(size_t count, size_t bytes, bool host) const {
     std::lock_guard<std::mutex> lk(slot_mu);
-    if (bytes > slot_bytes) {
-        for (uint8_t *b : slot_bufs) (void)hipFree(b);
-        slot_bufs.clear();
-        slot_bytes = bytes;
+    std::vector<uint8_t *> &bufs = host ? host_slot_bufs : slot_bufs;
+    size_t &cap = host ? host_slot_bytes : slot_bytes;
+    if (bytes > cap) {
+        for (uint8_t *b : bufs) (void)(host ? hipHostFree(b) : hipFree(b));
+        bufs.clear();
+        cap = bytes;
     }
     BPG_HIP(hipSetDevice(device));
-    while (slot_bufs.size() < count) {
+    while (bufs.size() < count) {
         uint8_t *b = nullptr;
-        BPG_HIP(hipMalloc((void **)&b, slot_bytes));
-        slot_bufs.push_back(b);
+        if (host) BPG_HIP(hipHostMalloc((void **)&b, cap, hipHostMallocDefault));
+        else BPG_HIP(hipMalloc((void **)&b, cap));
+        bufs.push_back(b);
     }
-    return std::vector<uint8_t *>(slot_bufs.begin(), slot_bufs.begin() + count);
+    return std::vector<uint8_t *>(bufs.begin(), bufs.begin() + count);
 }
 
 PreparedCS::~PreparedCS() {
     for (uint8_t *b : slot_bufs) (void)hipFree(b);
+    for (uint8_t *b : host_slot_bufs) (void)hipHostFree(b);
     DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols};
     for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
 }
@@ -893,6 +897,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                                                      const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
     if (P < 1 || P > MAX_LOCKSTEP) throw std::runtime_error("lockstep proof count");
+    static_assert(16 * MAX_LOCKSTEP <= MSM_MAX_SEGS, "an IPP job holds up to 16 segments per proof");
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t n = cs.n, m = cs.m, N = cs.N, lgN = cs.lgN;
     // this rank's slice: lanes i = j * world + rank, j < nl real, j < Nl padded

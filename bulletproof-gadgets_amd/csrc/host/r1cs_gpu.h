@@ -103,11 +103,12 @@ struct PreparedCS {
     DBuf col_ptr, col_row, col_coeff, short_cols, long_cols;
     uint32_t nshort = 0, nlong = 0, ncol = 0;
     std::vector<uint32_t> huge_cols, col_ptr_host;
-    // pinned host buffers for batched RNG output (grow-only, reused)
+    // buffers for batched RNG output (grow-only, reused): device memory, or
+    // pinned host memory (host = true) that the consumer's stream copies up
     mutable std::mutex slot_mu;
-    mutable std::vector<uint8_t *> slot_bufs;
-    mutable size_t slot_bytes = 0;
-    std::vector<uint8_t *> slots(size_t count, size_t bytes) const;
+    mutable std::vector<uint8_t *> slot_bufs, host_slot_bufs;
+    mutable size_t slot_bytes = 0, host_slot_bytes = 0;
+    std::vector<uint8_t *> slots(size_t count, size_t bytes, bool host = false) const;
     ~PreparedCS();
 };
 
