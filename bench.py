@@ -399,6 +399,7 @@ def main():
         for r in rows[:48]:
             print("  %.2f %.2f %s %s" % r, file=sys.stderr)
     L.bpg_profile_enable(0)
+    free_b, total_b = torch.cuda.mem_get_info(dev)   # HBM in use after the run (tables + workspaces)
     if dist is not None:
         dt = D.max_over_ranks(dt)
 
@@ -484,6 +485,7 @@ def main():
                    "parallelism": "independent proofs per GPU (%d ranks)" % world,
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline"},
         "host_cores_busy": round(host_busy, 2),
+        "hbm_used_gb": round((total_b - free_b) / 1e9, 1),
         "latency_ms_single_proof": round(single_ms, 1),
         "cold_setup_ms": round(prepare_ms, 1),
         "cold_setup_breakdown_ms": {"generators": round(setup["gens_ms"], 1), "comb_tables": round(setup["comb_ms"], 1),

@@ -98,10 +98,12 @@ class MsmEngine {
     explicit MsmEngine(hipStream_t st) : st_(st) {}
     ~MsmEngine();
     // Enqueue a multi-MSM job on the stream; window-row sums land in
-    // `rows_host` (pinned, nmsm * W points) when `done` fires.
+    // `rows_host` (pinned, nmsm * W points) once the stream reaches this point.
+    // rows_direct: the device view of rows_host (hipHostGetDevicePointer);
+    // when given, the row kernel writes there and no copy is enqueued.
     // Returns the plan (window width c and count W are needed by the host
-    // combine). Segments: at most 12, all bases in format `fmt`.
-    MsmPlan enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt);
+    // combine). Segments: at most MSM_MAX_SEGS, all bases in format `fmt`.
+    MsmPlan enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt, PtD *rows_direct = nullptr);
   private:
     void reserve(const MsmPlan &p);
     hipStream_t st_;
@@ -155,8 +157,9 @@ struct IppRoundArgs {
 };
 // msm_scal[0..4h) = [aL*lamGf_R | bR*muHf_L | aR*lamGf_L | bL*muHf_R]; c_L -> msm_scal[4h],
 // c_R -> msm_scal[4h+1]
+// c_out: c_L, c_R (2 scalars; may be a device view of pinned host memory)
 void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
-                     ScD *partial, hipStream_t st);
+                     ScD *partial, ScD *c_out, hipStream_t st);
 void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st);
 // Ghat' = Ghat_L + rho * Ghat_R (rho = rho_a except lanes i < n <= h+i, which use rho_b)
 // Kernel-argument block staged through pinned host memory to a device buffer
@@ -212,7 +215,7 @@ struct LazyArgs {
 };
 // msm_scal[0..8h) (layout in kernels.hip), c_L -> [8h], c_R -> [8h+1]
 void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
-                          ScD *msm_scal, ScD *partial, hipStream_t st);
+                          ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st);
 // Round k+2 of a round triple (levels k+1, k+2 unmaterialised): each base
 // expanded into four level-k points. r1/r0: rounds k+1 / k fold scalars
 // (Montgomery) per vector (0 = G, 1 = H) and class (1: the pair straddles n).
@@ -221,7 +224,7 @@ struct Deep2Args {
 };
 // msm_scal[0..16h) (layout in kernels.hip), c_L -> [16h], c_R -> [16h+1]
 void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
-                           ScD *msm_scal, ScD *partial, hipStream_t st);
+                           ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st);
 // Three-round Straus fold from level k (NielsD at level 0, else PtD):
 // out_i = P_i + sum_{t=1..7} c_t P_{i + t hq}, i < hq; coef[v][r][t-1] canonical
 // for lanes [rstart[r], rstart[r+1]). `tab`: odd-multiple tables,
@@ -237,7 +240,7 @@ void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq,
 // scalars over that level: out = [sLG | sLH | sRG | sRH] (a point not in a
 // segment's half gets 0), c_L -> out[4M], c_R -> out[4M + 1].
 void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, uint32_t M,
-                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, hipStream_t st);
+                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, ScD *c_out, hipStream_t st);
 // after round k: w_j *= rho (Montgomery) for the upper half (j mod 2h >= h),
 // rho_b for the lanes whose pair straddles n
 void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t n, ScD rGa, ScD rGb, ScD rHa,

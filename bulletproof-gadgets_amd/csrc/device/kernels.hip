@@ -1197,7 +1197,7 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
     BPG_HIP(hipGetLastError());
 }
 
-MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt) {
+MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt, PtD *rows_direct) {
     if (nseg < 1 || nseg > MSM_MAXSEG) throw HipError(hipErrorInvalidValue, "nseg", __FILE__, __LINE__);
     if (fmt != MSM_NIELS && fmt != MSM_CACHED)
         throw HipError(hipErrorInvalidValue, "fmt", __FILE__, __LINE__);
@@ -1355,6 +1355,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         pout = a ? AS_GE(rp_b_.p) : AS_GE(rp_a_.p);
     }
     hipLaunchKernelGGL(k_rbk_final, dim3(nblk(E, 64)), dim3(64), 0, st_, kin, pin, E, invalid, p.c, buckets, bflag);
+    // the row kernel writes the window rows straight into the caller's pinned
+    // buffer when it gives a device view of it (no copy launch per job)
+    ge *rows_out = rows_direct ? reinterpret_cast<ge *>(rows_direct) : AS_GE(rows_dev_.p);
 #if ROW_TWO_LEVEL
     {
         // P threads per row (power of two), L buckets each, blocks of B <= 256
@@ -1365,10 +1368,10 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         while ((1u << lgBL) < B * L) lgBL++;
         ge *blkB = AS_GE(segacc_.p), *blkU = blkB + (size_t)p.rows * SB;
         hipLaunchKernelGGL(k_row_blocks, dim3(p.rows * SB), dim3(B), 0, st_, AS_CGE(buckets_.p), bflag,
-                           (uint32_t)p.half, L, lgL, SB, (uint32_t)nmsm, (uint32_t)p.W, blkB, blkU, AS_GE(rows_dev_.p));
+                           (uint32_t)p.half, L, lgL, SB, (uint32_t)nmsm, (uint32_t)p.W, blkB, blkU, AS_GE(rows_out));
         if (SB > 1)
             hipLaunchKernelGGL(k_row_final, dim3(p.rows), dim3(64), 0, st_, (const ge *)blkB, (const ge *)blkU, SB,
-                               lgBL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
+                               lgBL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out));
     }
 #else
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
@@ -1378,10 +1381,11 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     int lgL = 0;
     while ((1 << lgL) < p.seglen) lgL++;
     hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
-                       (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_dev_.p));
+                       (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out));
 #endif
     BPG_HIP(hipGetLastError());
-    BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
+    if (!rows_direct)
+        BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
     return p;
 }
 
@@ -1694,13 +1698,12 @@ __global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, cons
     block_reduce_store<2>(acc, partial);
 }
 void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
-                     ScD *partial, hipStream_t st) {
+                     ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
     hipLaunchKernelGGL(k_ipp_prep, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args,
                        AS_SC(msm_scal), AS_SC(partial));
-    // c_L -> msm_scal[4h], c_R -> msm_scal[4h+1]
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
-                       AS_SC(msm_scal + 4 * (size_t)args.h), 1u, 0);
+    // c_L -> c_out[0], c_R -> c_out[1]
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 // u, uinv in Montgomery form
@@ -2500,12 +2503,11 @@ __global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a,
     block_reduce_store<2>(acc, partial);
 }
 void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
-                          ScD *msm_scal, ScD *partial, hipStream_t st) {
+                          ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
     hipLaunchKernelGGL(k_ipp_prep_lazy, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, lz,
                        AS_SC(msm_scal), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
-                       AS_SC(msm_scal + 8 * (size_t)args.h), 1u, 0);
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 
@@ -2561,12 +2563,11 @@ __global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a
     block_reduce_store<2>(acc, partial);
 }
 void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
-                           ScD *msm_scal, ScD *partial, hipStream_t st) {
+                           ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
     hipLaunchKernelGGL(k_ipp_prep_deep2, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, z,
                        AS_SC(msm_scal), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u,
-                       AS_SC(msm_scal + 16 * (size_t)args.h), 1u, 0);
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a, const sc *__restrict__ b,
@@ -2612,12 +2613,11 @@ __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a,
     block_reduce_store<2>(acc, partial);
 }
 void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, uint32_t M,
-                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, hipStream_t st) {
+                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(M, 256)));
     hipLaunchKernelGGL(k_ipp_prep_tail, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, M,
                        AS_CSC(wG), AS_CSC(wH), AS_SC(out), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(out + 4 * (size_t)M),
-                       1u, 0);
+    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 __global__ void k_ipp_tail_weights(sc *__restrict__ wG, sc *__restrict__ wH, uint32_t M, uint32_t h, uint32_t n,

@@ -323,6 +323,7 @@ struct ProofBufs {
     DBuf wide, sL, sR, w, wloc, l1, r0, r1, r3, ypm, yipm, zlo, zhi, ylo, yhi, tabs, a, b, mscal, partial, Gp[2], Hp[2],
         small, wG, wH, wconv, f3tab;
     ScD *small_host = nullptr;   // pinned, 4096 scalars
+    ScD *small_view = nullptr;   // its device view (kernels write c_L, c_R there)
     dev::ArgStage fold_stage, comb_stage, fold2_stage, fold3_stage;
     ~ProofBufs() {
         for (dev::ArgStage *a : {&fold_stage, &comb_stage, &fold2_stage, &fold3_stage}) {
@@ -343,6 +344,7 @@ struct Workspace : dev::ProfSink {
     std::unique_ptr<MsmEngine> msm;
     DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag;
     PtD *rows_host = nullptr;        // pinned, 2 x ROWS_HALF window rows
+    PtD *rows_view = nullptr;        // its device view (the row kernels write there)
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
@@ -421,11 +423,19 @@ Workspace &thread_workspace(int device) {
         BPG_HIP(hipEventCreateWithFlags(&p->done_ev, hipEventBlockingSync | hipEventDisableTiming));
         p->msm.reset(new MsmEngine(p->st));
         BPG_HIP(hipHostMalloc((void **)&p->rows_host, 2 * ROWS_HALF * sizeof(PtD), hipHostMallocDefault));
+        BPG_HIP(hipHostGetDevicePointer((void **)&p->rows_view, p->rows_host, 0));
         BPG_HIP(hipHostMalloc((void **)&p->small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
     }
     dev::set_prof_sink(p.get());   // this thread's launches record on its own stream
     BPG_HIP(hipSetDevice(device));
     return *p;
+}
+
+// BPG_ZERO_COPY=0: copy the MSM rows and c_L / c_R down with hipMemcpyAsync
+// instead of writing them into pinned memory from the kernels (A/B switch)
+static bool zero_copy() {
+    static const bool on = [] { const char *e = getenv("BPG_ZERO_COPY"); return !(e && e[0] == '0'); }();
+    return on;
 }
 
 ProveTimings &last_timings() { static thread_local ProveTimings t; return t; }
@@ -913,16 +923,29 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     for (int p = 0; p < P; p++) {
         ProofBufs &B = ws.pb[p];
         B.tabs.grow(8 * 40 * sizeof(ScD));
-        if (!B.small_host) BPG_HIP(hipHostMalloc((void **)&B.small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
+        if (!B.small_host) {
+            BPG_HIP(hipHostMalloc((void **)&B.small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
+            BPG_HIP(hipHostGetDevicePointer((void **)&B.small_view, B.small_host, 0));
+        }
         T.push_back(prover_transcript(cs, label, label_len));
     }
 
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G>, S1 = <s_L,G> + <s_R,H>
     // (blinding terms added on the host): one MSM job, MSMs 3p .. 3p + 2
     PtD *rowsA = ws.rows_host, *rowsLR = ws.rows_host + ROWS_HALF;
+    // zero copy: the MSM row kernels and the c_L / c_R reductions write into
+    // the pinned buffers through their device views (no copy launch per job)
+    const bool zc = zero_copy();
+    PtD *rowsA_dev = zc ? ws.rows_view : nullptr, *rowsLR_dev = zc ? ws.rows_view + ROWS_HALF : nullptr;
     const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
     const int64_t gneg = gs->N;             // their negations follow each vector
-    MsmPlan pA{};
+    // one job for all P proofs' commitments, or one job per proof
+    // (BPG_LOCKSTEP_COMMIT=0, the default: a P-proof commitment job is the
+    // largest of the proof and sizes every workspace's MSM scratch — ~7 GB at
+    // P = 2 and 2^20 — so per-proof jobs leave HBM for more consumers)
+    static const bool one_commit_job = [] { const char *e = getenv("BPG_LOCKSTEP_COMMIT"); return e && e[0] == '1'; }();
+    const size_t ROWS_PER_PROOF = 192;   // 3 MSMs x at most 64 windows
+    MsmPlan pA[MAX_LOCKSTEP] = {};
     {
         MsmSeg seg[5 * MAX_LOCKSTEP];
         int nseg = 0;
@@ -949,10 +972,19 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             seg[nseg++] = {as<ScD>(B.sL), G0, nl, m0 + 2, gneg};
             seg[nseg++] = {as<ScD>(B.sR), H0, nl, m0 + 2, gneg};
         }
-        if (nseg) {
+        if (nseg && (one_commit_job || P == 1)) {
             int ph = ws.prof_begin("msm_commit", 5.0 * P * nl * (64 + 32));
-            pA = ws.msm->enqueue(seg, nseg, 3 * P, rowsA, MSM_NIELS);
+            pA[0] = ws.msm->enqueue(seg, nseg, 3 * P, rowsA, MSM_NIELS, rowsA_dev);
             ws.prof_end(ph);
+            for (int p = 1; p < P; p++) pA[p] = pA[0];
+        } else if (nseg) {
+            for (int p = 0; p < P; p++) {
+                for (int k = 0; k < 5; k++) seg[5 * p + k].msm -= 3 * (uint32_t)p;
+                int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
+                pA[p] = ws.msm->enqueue(seg + 5 * p, 5, 3, rowsA + ROWS_PER_PROOF * p, MSM_NIELS,
+                                        rowsA_dev ? rowsA_dev + ROWS_PER_PROOF * p : nullptr);
+                ws.prof_end(ph);
+            }
         }
     }
     ws.sync();
@@ -962,7 +994,9 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         const RngBlock &rb = *rbs[p];
         Point AIS[3], tmp;
         if (nl) {
-            for (int k = 0; k < 3; k++) combine_rows(AIS[k], rowsA + (3 * p + k) * pA.W, pA.W, pA.c);
+            const MsmPlan &pl = pA[p];
+            const PtD *rows = (one_commit_job || P == 1) ? rowsA + 3 * p * pl.W : rowsA + ROWS_PER_PROOF * p;
+            for (int k = 0; k < 3; k++) combine_rows(AIS[k], rows + k * pl.W, pl.W, pl.c);
         } else {
             pt_identity(AIS[0]); pt_identity(AIS[1]); pt_identity(AIS[2]);
         }
@@ -1026,7 +1060,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         }
         for (DBuf *d : {&B.l1, &B.r0, &B.r1, &B.r3}) d->grow((size_t)nl * sizeof(ScD) + 64);
         B.small.grow(64 * sizeof(ScD));
-        ScD *dsmall = as<ScD>(B.small);
+        ScD *dsmall = zc ? B.small_view + 1000 : as<ScD>(B.small);   // t_1..t_6, <w_V, v_blinding>
         if (nl) {
             launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(B.sR), wL,
                             wR, wO, as<ScD>(B.ypm), as<ScD>(B.yipm), nl, as<ScD>(B.l1), as<ScD>(B.r0), as<ScD>(B.r1),
@@ -1038,7 +1072,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         }
         if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(B.partial), dsmall + 6, st);
         else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
-        BPG_HIP(hipMemcpyAsync(B.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
+        if (!zc) BPG_HIP(hipMemcpyAsync(B.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
     }
     ws.sync();
     std::vector<Scalar> u(P), x(P), t_x(P), t_xb(P), e_bl(P), wch(P);
@@ -1161,7 +1195,6 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         const size_t hh = h;
         MsmSeg seg[MSM_MAX_SEGS];
         int nseg = 0;
-        size_t cofs = 0;   // c_L, c_R at mscal[cofs], [cofs + 1]
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             IppRoundArgs A;
@@ -1169,24 +1202,24 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             A.lamG1 = mont(lam[p]); A.lamGu = mont(lam[p] * u[p]);
             A.muH1 = mont(mu[p]); A.muHu = mont(mu[p] * u[p]);
             ScD *ms = as<ScD>(B.mscal);
+            ScD *cout = zc ? B.small_view + 1020 : as<ScD>(B.small) + 60;   // c_L, c_R
             const void *Gm = cur < 0 ? G0 : Gh[p], *Hm = cur < 0 ? H0 : Hh[p];
             const uint32_t L0 = 2 * (uint32_t)p, R0 = L0 + 1;   // this proof's L and R MSMs
             if (tail) {
                 launch_ipp_prep_tail(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, M, as<ScD>(B.wG),
-                                     as<ScD>(B.wH), ms, as<ScD>(B.partial), st);
+                                     as<ScD>(B.wH), ms, as<ScD>(B.partial), cout, st);
                 const size_t mm_ = M;
                 seg[nseg++] = {ms, Gh[p], M, L0};
                 seg[nseg++] = {ms + mm_, Hh[p], M, L0};
                 seg[nseg++] = {ms + 2 * mm_, Gh[p], M, R0};
                 seg[nseg++] = {ms + 3 * mm_, Hh[p], M, R0};
-                cofs = 4 * mm_;
             } else if (lazy) {
                 const uint32_t h0 = 2 * h;
                 LazyArgs Z;
                 Z.h0 = h0;
                 Z.rGa = mont(rho_h[p][0][0]); Z.rGb = mont(rho_h[p][0][1]);
                 Z.rHa = mont(rho_h[p][0][2]); Z.rHb = mont(rho_h[p][0][3]);
-                launch_ipp_prep_lazy(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), st);
+                launch_ipp_prep_lazy(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), cout, st);
                 seg[nseg++] = {ms, at(Gm, h), h, L0, gn};
                 seg[nseg++] = {ms + hh, at(Gm, h + h0), h, L0, gn};
                 seg[nseg++] = {ms + 2 * hh, Hm, h, L0, gn};
@@ -1195,7 +1228,6 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                 seg[nseg++] = {ms + 5 * hh, at(Gm, h0), h, R0, gn};
                 seg[nseg++] = {ms + 6 * hh, at(Hm, h), h, R0, gn};
                 seg[nseg++] = {ms + 7 * hh, at(Hm, h + h0), h, R0, gn};
-                cofs = 8 * hh;
             } else if (depth == 2) {
                 // bases at level k+2 expanded into level k: family f, term t at
                 // out[(4f + t) h], point offset x0(f) + 2h t
@@ -1205,7 +1237,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                         Z.r0[v][c] = mont(rho_h[p][0][2 * v + c]);
                         Z.r1[v][c] = mont(rho_h[p][1][2 * v + c]);
                     }
-                launch_ipp_prep_deep2(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), st);
+                launch_ipp_prep_deep2(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), cout, st);
                 for (int f = 0; f < 4; f++) {
                     const void *Bs = (f & 1) ? Hm : Gm;
                     const size_t x0 = (f == 0 || f == 3) ? hh : 0;
@@ -1213,21 +1245,19 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                         seg[nseg++] = {ms + (size_t)(4 * f + t) * hh, at(Bs, x0 + 2 * hh * t), h,
                                        (uint32_t)(f >> 1) + L0, gn};
                 }
-                cofs = 16 * hh;
             } else {
-                launch_ipp_prep(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, ms, as<ScD>(B.partial), st);
+                launch_ipp_prep(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, ms, as<ScD>(B.partial), cout, st);
                 // points whose a-scalar is zero (padding lanes) are left out of
                 // the job: L's G part runs over a_lo, R's over a_hi
                 const uint32_t nLG = std::min(h, anz), nRG = anz > h ? std::min(h, anz - h) : 0u;
                 const MsmSeg sl[4] = {{ms, at(Gm, h), nLG, L0, gn}, {ms + hh, Hm, h, L0, gn},
                                       {ms + 2 * hh, Gm, nRG, R0, gn}, {ms + 3 * hh, at(Hm, h), h, R0, gn}};
                 for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
-                cofs = 4 * hh;
             }
-            BPG_HIP(hipMemcpyAsync(B.small_host + 1020, ms + cofs, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
+            if (!zc) BPG_HIP(hipMemcpyAsync(B.small_host + 1020, cout, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
         }
         int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));
-        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt);
+        MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt, rowsLR_dev);
         ws.prof_end(ph);
         ws.sync();
         std::vector<std::array<Scalar, 4>> rnow(P);   // this round's fold scalars (G a/b, H a/b)
