@@ -48,10 +48,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 16 x threads)")
+    ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 24 x threads)")
     ap.add_argument("--threads", type=int, default=0,
-                    help="host threads per GPU: a third draw the TranscriptRng streams (at most 8), the rest drive "
-                         "one HIP stream each (default 24 with >= 16 cpus)")
+                    help="host threads per GPU: half draw the TranscriptRng streams (at most 8), the rest drive "
+                         "one HIP stream each, two proofs at a time (default 16 with >= 16 cpus; verify mode 24)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
@@ -93,10 +93,10 @@ def pmc_row(kernel):
 
 def prof_row(kernel):
     """The average duration (us) and launch count of `kernel` in the latest
-    committed rocprofv3 --kernel-trace --stats table of the default 24-thread
-    bench (profiles/*_prof24_kernels.md, scripts/prof_summary.py), or {}."""
+    committed rocprofv3 --kernel-trace --stats table of the bench's default
+    command (profiles/*_profdefault_kernels.md, scripts/prof_summary.py), or {}."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_prof24_kernels.md")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_profdefault_kernels.md")))
     if not files:
         return {}
     for line in open(files[-1]):
@@ -323,14 +323,19 @@ def main():
     global DIST_INFO
     DIST_INFO = dist_info(torch, dist, D, dev, world)
     ncpu = job_cpus()
-    # consumers mostly sleep on the device (event polls), so 24 threads keep
-    # ~9 host cores busy: 8 RNG producers + 16 streams
+    # consumers mostly sleep on the device (event polls), so 16 threads keep
+    # ~3-9 host cores busy: 8 RNG producers + 8 device streams, each stream
+    # proving two proofs at once (bpg_prove_batch's default lockstep)
     per_rank = ncpu // max(world, 1) if world > 1 else ncpu
-    threads = a.threads or max(1, min(24, per_rank * 3 // 2))
+    # (host_cores_busy ~3.2 at 16 threads, so a rank may run 4 threads per CPU of its share)
+    threads = a.threads or max(1, min(16, per_rank * 4))
+    if a.mode == "verify" and not a.threads:
+        threads = max(1, min(24, per_rank * 3 // 2))   # one HIP stream per verifying thread
     threads = min(threads, 64)
-    # 16 proofs per host thread per step; the timed steps run as one
-    # continuous pipeline (below), so the end-of-batch drain is paid once
-    batch = a.batch or 16 * threads
+    # 384 proofs per step (24 per host thread at the default 16); the timed
+    # steps run as one continuous pipeline (below), so the end-of-batch drain
+    # is paid once
+    batch = a.batch or 24 * threads
 
     if a.mode == "statements":
         return bench_statements(a, bpg, dist, D, rank, world, W)
@@ -458,9 +463,9 @@ def main():
                                  if k in ("avg_us", "valu_issue_share", "avg_waves_per_simd", "wave_wait_mem",
                                           "hbm_gbs", "clock_ghz", "source")} or None,
                 # the same kernel's average launch in the committed rocprofv3
-                # kernel trace of this command (24 host threads), and the HBM
-                # fraction that average gives
-                "rocprof_24threads": dict(prof, frac=round((by / lc) / (prof["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 6))
+                # kernel trace of this command (default host threads), and the
+                # HBM fraction that average gives
+                "rocprof_default_cmd": dict(prof, frac=round((by / lc) / (prof["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 6))
                 if prof else None,
                 "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
                 "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items() if v}}

@@ -298,6 +298,10 @@ int bpg_prove_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len,
 /* Prove `count` independent proofs of one prepared circuit (proof k uses
  * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
  * host threads sharing the device. lens[k] receives each proof length.
+ * Half of the threads (at most 8) draw the TranscriptRng streams, 8 proofs
+ * at a time; each of the others proves two proofs at once on its own HIP
+ * stream, their MSM jobs merged (BPG_LOCKSTEP=1: one proof per stream, a
+ * third of the threads drawing). Proof bytes do not depend on either.
  * Batch calls (this and bpg_verify_batch) run on one process-wide worker
  * pool: concurrent calls from several threads are safe and run one after
  * the other. */
