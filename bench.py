@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 24 x threads)")
     ap.add_argument("--threads", type=int, default=0,
                     help="host threads per GPU: half draw the TranscriptRng streams (at most 8), the rest drive "
-                         "one HIP stream each, two proofs at a time (default 16 with >= 16 cpus; verify mode 24)")
+                         "one HIP stream each, four proofs at a time, at most 24 proofs in flight at 2^20 "
+                         "(default 16 with >= 4 cpus; verify mode 24)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
@@ -324,8 +325,9 @@ def main():
     DIST_INFO = dist_info(torch, dist, D, dev, world)
     ncpu = job_cpus()
     # consumers mostly sleep on the device (event polls), so 16 threads keep
-    # ~3-9 host cores busy: 8 RNG producers + 8 device streams, each stream
-    # proving two proofs at once (bpg_prove_batch's default lockstep)
+    # ~3 host cores busy: 8 RNG producers + 6 device streams, each proving
+    # four proofs at once (bpg_prove_batch's default lockstep; its in-flight
+    # cap for HBM leaves the other 2 threads unused at 2^20)
     per_rank = ncpu // max(world, 1) if world > 1 else ncpu
     # (host_cores_busy ~3.2 at 16 threads, so a rank may run 4 threads per CPU of its share)
     threads = a.threads or max(1, min(16, per_rank * 4))

@@ -435,8 +435,11 @@ DEVI void gec_neg(gec &r, const gec &c) { r.YpX = c.YmX; r.YmX = c.YpX; r.Z2 = c
 DEVI void gec_cneg(gec &c, bool neg) {
     if (neg) { fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; fe_neg(c.T2d, c.T2d); }
 }
-// add-2008-hwcd-3 (a = -1) with a cached right operand: 8M
-DEVI void ge_add_c(ge &r, const ge &p, const gec &q) {
+// add-2008-hwcd-3 (a = -1) with a cached right operand: 8M; with_t = false
+// skips T (7M) for an addition followed by a doubling (T is not an input of
+// doubling), as ge_dbl_t does.
+template <bool with_t>
+DEVI void ge_add_c_t(ge &r, const ge &p, const gec &q) {
     fe a, b, c, d, e, f, g, h;
     fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q.YmX);       // 3T x T
     fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q.YpX);       // 2T x T
@@ -446,9 +449,10 @@ DEVI void ge_add_c(ge &r, const ge &p, const gec &q) {
     fe_sub_nc(f, d, c);                                 // 3T
     fe_add_nc(g, d, c);                                 // 2T
     fe_add_nc(h, b, a);                                 // 2T
-    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); if (with_t) fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
 }
-DEVI void ge_sub_c(ge &r, const ge &p, const gec &q) {
+template <bool with_t>
+DEVI void ge_sub_c_t(ge &r, const ge &p, const gec &q) {
     fe a, b, c, d, e, f, g, h;
     fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q.YpX);
     fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q.YmX);
@@ -458,8 +462,10 @@ DEVI void ge_sub_c(ge &r, const ge &p, const gec &q) {
     fe_add_nc(f, d, c);                                 // D + C for -q
     fe_sub_nc(g, d, c);
     fe_add_nc(h, b, a);
-    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); if (with_t) fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
 }
+DEVI void ge_add_c(ge &r, const ge &p, const gec &q) { ge_add_c_t<true>(r, p, q); }
+DEVI void ge_sub_c(ge &r, const ge &p, const gec &q) { ge_sub_c_t<true>(r, p, q); }
 // madd-2008-hwcd-3 (a = -1) with an affine Niels right operand: 7M.
 // D = 2 Z1 unreduced (2T): F = D - C <= 4T, G = D + C <= 3T, E <= 3T,
 // H <= 2T, so every product below keeps fe_mul's argument bounds.

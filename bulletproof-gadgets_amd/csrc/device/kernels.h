@@ -63,7 +63,7 @@ void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count,
 
 // -------------------------------------------------------------- MSM
 #ifndef MSM_MAX_SEGS
-#define MSM_MAX_SEGS 32   // segments per MSM job (two lockstep proofs of a round-triple IPP job: 2 x 16); the 5-bit segment field of an entry holds 0..31
+#define MSM_MAX_SEGS 64   // segments per MSM job (four lockstep proofs of a round-triple IPP job: 4 x 16); the 6-bit segment field of an entry holds 0..63
 #endif
 #define MSM_CACHED 0   // bases are cached points (PtD)
 #define MSM_NIELS 1    // bases are affine Niels points (NielsD)

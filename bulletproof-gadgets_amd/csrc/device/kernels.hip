@@ -210,17 +210,21 @@ struct SegTab {
     uint32_t row0[MSM_MAXSEG];
     int n;
 };
-// val = sign << 31 | segment << 26 | point index within the segment: the
+// val = sign << 31 | segment << 25 | point index within the segment: the
 // digit kernel resolves the segment once per point, so the run reduction
 // gathers from a per-block pointer table in LDS without searching segments
-#define MSM_SEG_SHIFT 26
+#define MSM_SEG_SHIFT 25
 #define MSM_LOC_MASK ((1u << MSM_SEG_SHIFT) - 1)
-static_assert(MSM_MAXSEG <= 32, "an entry's segment field is 5 bits");
-DEVI int seg_of(const SegTab &T, uint32_t g) {
-    int si = 0;
-#pragma unroll
-    for (int k = 1; k < MSM_MAXSEG; k++) if (k < T.n && g >= T.gofs[k]) si = k;
-    return si;
+static_assert(MSM_MAXSEG <= 64, "an entry's segment field is 6 bits");
+// the segment holding point g: the last k < n with gofs[k] <= g (gofs[0] = 0;
+// gofs staged in LDS by the caller)
+DEVI int seg_of(const uint32_t *gofs, int n, uint32_t g) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (g >= gofs[mid]) lo = mid; else hi = mid - 1;
+    }
+    return lo;
 }
 
 // Signed c-bit windows. Entry of (point g, window w): key = row << c | slot,
@@ -233,17 +237,21 @@ DEVI int seg_of(const SegTab &T, uint32_t g) {
 // tile table (5 words per tile: start, end, first tile of the row, one past
 // its last, row start; then each row's first tile), computed from the job's
 // geometry instead of being built on the host and copied up per job.
+#define TILEGEO_MAXMSM 8   // MSMs of a job whose tile table the digit launch writes (4 lockstep proofs' L and R)
 struct TileGeo {
     uint32_t nt, rows, tile, TW;      // tiles, rows, entries per tile, tiles per window
-    uint32_t moff[4], mtot[4], tpr[4], cum[4];
+    uint32_t moff[TILEGEO_MAXMSM], mtot[TILEGEO_MAXMSM], tpr[TILEGEO_MAXMSM], cum[TILEGEO_MAXMSM];
     uint8_t *bflag;                   // cleared: bflag_bytes (multiple of 16)
     uint64_t bflag_bytes;
     uint32_t *tiles;                  // null: the host wrote the table
 };
 __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G) {
+    __shared__ uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
+    if (threadIdx.x <= (uint32_t)T.n) gofs[threadIdx.x] = T.gofs[threadIdx.x];
+    __syncthreads();
     for (uint64_t q = g; q < G.bflag_bytes / 16; q += stride) reinterpret_cast<uint4 *>(G.bflag)[q] = uint4{0, 0, 0, 0};
     if (G.tiles) {
         for (uint32_t x = g; x < G.nt + G.rows; x += stride) {
@@ -267,7 +275,7 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
         }
     }
     if (g >= total) return;
-    int si = seg_of(T, g);
+    int si = seg_of(gofs, T.n, g);
     sc k;
     sc_load(k, T.scal[si] + (g - T.gofs[si]));
     uint32_t carry = 0, mask = (1u << c) - 1, full = 1u << c;
@@ -644,7 +652,7 @@ DEVI void pt_load_global(P &p, uint64_t addr) {
 }
 template <int FMT, bool NEGC>
 DEVI void msm_load_base(typename BaseOf<FMT>::T &p, const uint64_t *sptr, uint32_t v) {
-    const uint32_t si = (v >> MSM_SEG_SHIFT) & 31u;
+    const uint32_t si = (v >> MSM_SEG_SHIFT) & 63u;
     const uint32_t sel = NEGC ? (v >> 31) * MSM_MAXSEG + si : si;
     pt_load_global(p, sptr[sel] + (uint64_t)(v & MSM_LOC_MASK) * sizeof(typename BaseOf<FMT>::T));
 }
@@ -878,7 +886,17 @@ __global__ __launch_bounds__(64, BPG_LAT_WAVES) void k_rbk_final(const uint32_t 
 DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict__ F, size_t i) {
     if (F[i]) ge_load(p, B + i); else ge_identity(p);
 }
-__global__ __launch_bounds__(64, 3) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
+// Registers of the bucket-row kernels: they hold CUs next to the VALU-bound
+// kernels of other streams for up to a millisecond, so every register they do
+// not need is room for another wave of those (ROW_WAVES / BSEG_WAVES: waves
+// per SIMD compiled for).
+#ifndef BSEG_WAVES
+#define BSEG_WAVES 3
+#endif
+#ifndef ROW_WAVES
+#define ROW_WAVES 1
+#endif
+__global__ __launch_bounds__(64, BSEG_WAVES) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
                                                    uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
                                                    ge *__restrict__ segA, ge *__restrict__ segT) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -907,7 +925,7 @@ DEVI void ge_dbl_n(ge &r, int n) {
 // Rows are numbered window-major (row = w * nmsm + msm); results land at
 // msm * W + w, the layout the host combine reads.
 DEVI uint32_t row_perm(uint32_t row, uint32_t nmsm, uint32_t W) { return (row % nmsm) * W + row / nmsm; }
-__global__ __launch_bounds__(256) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
+__global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
                                                     uint32_t nseg, int lgL, uint32_t nmsm, uint32_t W,
                                                     ge *__restrict__ rows_out) {
     __shared__ ge sh[256];
@@ -1248,7 +1266,16 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     p.key_bits = (uint32_t)p.c;   // the sort orders slots within rows
     // slots after pass 1: two per thread chunk, padded to whole blocks
     p.capE = 2 * ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
-    p.seglen = p.half < 8 ? p.half : 8;
+    // buckets per first-level segment (k_bucket_seg): a row of `half`
+    // buckets leaves half / seglen segments for the one-block row reduction,
+    // whose serial part is 3 additions per segment per thread
+    // (BPG_MSM_SEGLEN, a power of two; A/B)
+    static const uint32_t seg_cfg = [] {
+        const char *e = getenv("BPG_MSM_SEGLEN");
+        const uint32_t v = e ? (uint32_t)atoi(e) : 8u;
+        return v >= 2 && v <= 256 && (v & (v - 1)) == 0 ? v : 8u;
+    }();
+    p.seglen = p.half < seg_cfg ? p.half : seg_cfg;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
         for (int r = 0; r < p.rows; r++) {
@@ -1269,7 +1296,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     geo.bflag = bflag;
     geo.bflag_bytes = (D + 15) / 16 * 16;   // bflag_ holds D + D/4 + 256 bytes
     uint32_t nt = 0;
-    if (nmsm <= 4) {   // the digit launch writes the tile table
+    if (nmsm <= TILEGEO_MAXMSM) {   // the digit launch writes the tile table
         for (int m = 0; m < nmsm; m++) {
             geo.moff[m] = moff[m];
             geo.mtot[m] = mtot[m];
@@ -1827,7 +1854,13 @@ __global__ __launch_bounds__(64, BPG_FOLD_WAVES) void k_ipp_fold_points(const Fo
         ge_dbl_t<true>(acc, acc);
         const int dk = S.dig[k];
         gec t; fold_pick(t, t1, t3, t5, t7, dk);
-        if (dk > 0) ge_add_c(acc, acc, t); else ge_sub_c(acc, acc, t);
+        // NAF digits are at least one doubling apart: T only for the last
+        // addition when no doubling follows it
+        if (k + 1 == S.ndig && S.tail == 0) {
+            if (dk > 0) ge_add_c_t<true>(acc, acc, t); else ge_sub_c_t<true>(acc, acc, t);
+        } else {
+            if (dk > 0) ge_add_c_t<false>(acc, acc, t); else ge_sub_c_t<false>(acc, acc, t);
+        }
     }
     if (S.tail) {
         for (uint32_t j = 1; j < S.tail; j++) ge_dbl_t<false>(acc, acc);
@@ -2009,7 +2042,12 @@ __global__ __launch_bounds__(64, WN == 3 ? 1 : 2) void k_ipp_fold2(const Fold2Ar
         }
         gec c;
         fold2_pick<WN>(c, tp, (op >> 8) & 3, (op >> 10) & 31);
-        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
+        // T only when another addition follows directly (wave-uniform)
+        if ((k + 1 < nops ? (fold2_op(ops, k + 1) & 255) : A.tail[sg]) == 0) {
+            if (op >> 15) ge_sub_c_t<true>(acc, acc, c); else ge_add_c_t<true>(acc, acc, c);
+        } else {
+            if (op >> 15) ge_sub_c_t<false>(acc, acc, c); else ge_add_c_t<false>(acc, acc, c);
+        }
     }
     const uint32_t tail = A.tail[sg];
     if (tail) {
@@ -2183,6 +2221,7 @@ __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *
 #if FOLD3_PREFETCH
     gec c;
     if (nops > 1) foldn_get(c, entry(fold2_op(ops, 1)));
+    const uint32_t tail = A.tail[sg];
     for (uint32_t k = 1; k < nops; k++) {
         const uint32_t op = fold2_op(ops, k);
         const uint32_t g = op & 255;
@@ -2192,6 +2231,9 @@ __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *
             for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
             ge_dbl_t<true>(acc, acc);
         }
+        // (skipping T before a doubling, as k_ipp_fold2 does, measured 4%
+        // slower here: 7.6 vs 7.3 s of bracketed fold time per step,
+        // profiles/r03j_ab_tskip_seglen.txt)
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
         c = cn;
     }
@@ -2209,8 +2251,8 @@ __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *
         foldn_get(c, entry(op));
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
     }
-#endif
     const uint32_t tail = A.tail[sg];
+#endif
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
         ge_dbl_t<true>(acc, acc);

@@ -388,26 +388,40 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
         if (threads == 0) threads = 1;
         uint32_t groups = (count + 7) / 8;
-        // proofs per consumer step (BPG_LOCKSTEP, 1 or 2; default 2: two
-        // proofs' MSM jobs merged, 81.4 / 80.7 vs 75.9 / 70.5 M constraints/s
-        // at one proof per step, profiles/r03h_ab_lockstep_consumers.txt)
+        // proofs per consumer step (BPG_LOCKSTEP, 1 to 4; default 4: the
+        // proofs' IPP MSM jobs merged, so the latency-bound launches after
+        // each job's first pass run once per four proofs. Measured at 24
+        // proofs in flight: 82.9 / 83.2 M constraints/s against 81.3 / 81.0
+        // for two per step and 75.9 / 70.5 for one,
+        // profiles/r03k_ab_lockstep4.txt, r03h_ab_lockstep_consumers.txt)
         static const int lockstep = [] {
             const char *e = getenv("BPG_LOCKSTEP");
-            const int v = e ? atoi(e) : 2;
-            return v >= 2 ? 2 : 1;
+            const int v = e ? atoi(e) : 4;
+            return v < 1 ? 1 : v > 4 ? 4 : v;
         }();
         // producers: at most 8 (one lockstep group of 8 each); slots (device
         // buffers) for the groups being drawn plus a queue per consumer. A
         // producer draws ~20 proofs/s. One proof per consumer step: a third of
-        // the threads (24 -> 8 producers, 16 consumers); two: half of them
-        // (16 -> 8 producers, 8 consumers, each proving two proofs at once)
+        // the threads (24 -> 8 producers, 16 consumers); more: half of them
+        // (16 -> 8 producers, 8 consumers)
         uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(groups, 8u),
-                                                              lockstep == 2 ? threads / 2 : threads / 3));
+                                                              lockstep >= 2 ? threads / 2 : threads / 3));
         if (const char *e = getenv("BPG_PRODUCERS")) {   // tuning override
             int v = atoi(e);
             if (v >= 1 && (uint32_t)v < threads) P = std::min<uint32_t>(groups, (uint32_t)v);
         }
         uint32_t C = std::max<uint32_t>(1, std::min<uint32_t>(count, threads > P ? threads - P : 1));
+        // proofs in flight, capped for HBM: a proof in flight holds ~3.1 GB
+        // at N = 2^20 (its buffers and its share of its stream's MSM
+        // scratch), next to 208 GB of comb tables: 24 of them keep the device
+        // at 292 GB of its 309 (BPG_MAX_INFLIGHT overrides; scales with 1/N)
+        static const uint32_t inflight_2p20 = [] {
+            const char *e = getenv("BPG_MAX_INFLIGHT");
+            const int v = e ? atoi(e) : 24;
+            return (uint32_t)(v < 1 ? 1 : v);
+        }();
+        const uint64_t inflight = std::max<uint64_t>(1, ((uint64_t)inflight_2p20 << 20) / std::max<uint32_t>(cs.N, 1));
+        C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(C, inflight / (uint64_t)lockstep));
         uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
         // BPG_HOST_SLOTS=1: producers write the draws into pinned host slots
         // and each consumer copies its proof's draws up on its own stream, so
@@ -469,7 +483,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                     // on its stream (gpu_prove_lockstep: one MSM job per step
                     // for all of them)
                     for (;;) {
-                        uint32_t ks[2];
+                        uint32_t ks[4];
                         int nk = 0;
                         {
                             std::unique_lock<std::mutex> lk(mu);
@@ -480,8 +494,8 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                                 ready.pop_front();
                             }
                         }
-                        const RngBlock *rbs[2];
-                        ProveTimings tms[2];
+                        const RngBlock *rbs[4];
+                        ProveTimings tms[4];
                         for (int i = 0; i < nk; i++) rbs[i] = &blocks[ks[i]];
                         std::vector<std::vector<uint8_t>> prs = gpu_prove_lockstep(cs, label, label_len, rbs, nk, tms);
                         for (int i = 0; i < nk; i++) {

@@ -317,7 +317,7 @@ void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_st
 // ---------------------------------------------------------------- workspace
 // Per-proof device buffers of the prover: a workspace drives up to
 // MAX_LOCKSTEP proofs of one circuit in lockstep (gpu_prove_lockstep).
-static const int MAX_LOCKSTEP = 2;
+static const int MAX_LOCKSTEP = 4;
 static const size_t ROWS_HALF = 1024;   // pinned MSM row buffer: commitments [0, 1024), IPP L/R [1024, 2048)
 struct ProofBufs {
     DBuf wide, sL, sR, w, wloc, l1, r0, r1, r3, ypm, yipm, zlo, zhi, ylo, yhi, tabs, a, b, mscal, partial, Gp[2], Hp[2],

@@ -299,9 +299,12 @@ int bpg_prove_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len,
  * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
  * host threads sharing the device. lens[k] receives each proof length.
  * Half of the threads (at most 8) draw the TranscriptRng streams, 8 proofs
- * at a time; each of the others proves two proofs at once on its own HIP
- * stream, their MSM jobs merged (BPG_LOCKSTEP=1: one proof per stream, a
- * third of the threads drawing). Proof bytes do not depend on either.
+ * at a time; each of the others proves four proofs at once on its own HIP
+ * stream, their IPP MSM jobs merged (BPG_LOCKSTEP=1..4; 1: one proof per
+ * stream, a third of the threads drawing). At most 24 * 2^20 / N proofs are
+ * in flight (HBM: ~3.1 GB each at N = 2^20 next to the comb tables;
+ * BPG_MAX_INFLIGHT), so extra threads stay idle. Proof bytes do not depend
+ * on any of this.
  * Batch calls (this and bpg_verify_batch) run on one process-wide worker
  * pool: concurrent calls from several threads are safe and run one after
  * the other. */

@@ -1,5 +1,5 @@
 #!/bin/bash
-# End-of-round check B: the default 24-thread bench under rocprofv3
+# End-of-round check B: the default bench command under rocprofv3
 # --kernel-trace --stats (kernel table + occupancy timeline; the bench's own
 # HIP-event bracketing on), the PMC passes of the current build (one counter
 # group per pass, kernel trace only), then the secondary modes.
@@ -7,11 +7,11 @@ set -o pipefail
 mkdir -p gpurun_out
 R=${R:-r03z}
 ROOTD=$(pwd)
-(cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/${R}_prof24 && \
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/${R}_prof24 -o run -- python3 $ROOTD/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $ROOTD/gpurun_out/${R}_prof24_bench.json 2> $ROOTD/gpurun_out/${R}_prof24.err) || exit $?
-db=$(find /tmp/${R}_prof24 -name '*.db' -print -quit)
-python3 scripts/prof_summary.py "$db" gpurun_out/${R}_prof24_kernels.md > /dev/null || exit $?
-python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline24.md 0.92 > /dev/null || exit $?
+(cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/${R}_prof && \
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/${R}_prof -o run -- python3 $ROOTD/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $ROOTD/gpurun_out/${R}_profdefault_bench.json 2> $ROOTD/gpurun_out/${R}_profdefault.err) || exit $?
+db=$(find /tmp/${R}_prof -name '*.db' -print -quit)
+python3 scripts/prof_summary.py "$db" gpurun_out/${R}_profdefault_kernels.md > /dev/null || exit $?
+python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline_default.md 0.92 > /dev/null || exit $?
 R=${R} ARGS="--steps 1 --warmup 1 --threads 8 --batch 32 --no-cpu-baseline" bash scripts/r02_pmc.sh || exit $?
 python3 scripts/pmc_table.py gpurun_out/${R} gpurun_out/${R}_pmc.json > gpurun_out/${R}_pmc_table.md || exit $?
 timeout -k 10 300 python bench.py --mode verify --steps 3 --warmup 1 > gpurun_out/${R}_verify.json 2> gpurun_out/${R}_verify.err || exit $?

@@ -24,7 +24,8 @@ void sim_sc_sub(const uint32_t *a, const uint32_t *b, uint32_t *r) { sc x, y, z;
 void sim_sc_reduce(const uint32_t *a, uint32_t *r) { sc x, z; memcpy(x.v, a, 32); sc_reduce(z, x); memcpy(r, z.v, 32); }
 // points: compressed in/out. op: 0 add, 1 sub, 2 add_cached, 3 sub_cached,
 // 4 dbl, 5 dbl without T then add (exercises the T-less doubling),
-// 9-12 identity-free run starts (Niels / cached -> extended, then + p)
+// 9-12 identity-free run starts (Niels / cached -> extended, then + p),
+// 13/14 (p +/- q without T) doubled, then + q (the folds' T-less additions)
 int sim_pt_op(int op, const uint32_t *a, const uint32_t *b, uint32_t *r) {
     ge p, q, s;
     if (!ristretto_decode(p, a) || !ristretto_decode(q, b)) return -1;
@@ -51,6 +52,8 @@ int sim_pt_op(int op, const uint32_t *a, const uint32_t *b, uint32_t *r) {
             gec c2 = qc; gec_cneg(c2, op == 12);
             ge t; ge_from_cached_t(t, c2); ge_add(s, t, p); break;
         }
+        case 13: { ge t; ge_add_c_t<false>(t, p, qc); ge_dbl(t, t); ge_add_c(s, t, qc); break; }   // T-less add, then dbl
+        case 14: { ge t; ge_sub_c_t<false>(t, p, qc); ge_dbl(t, t); ge_add_c(s, t, qc); break; }
         default: {          // Niels -> cached (2Z = 2) path of the fold kernel
             gen qn; ge_to_niels(qn, q); gec c2; gen_to_cached(c2, qn); ge_add_c(s, p, c2); break;
         }

@@ -140,8 +140,10 @@ def test_point_formulas_vs_oracle(sim):
         sub = O.point_add(a, O.point_mul(neg1, b))
         dbl = O.point_mul(two, a)
         four_plus = O.point_add(O.point_mul((4).to_bytes(32, "little"), a), b)
+        two_add_plus = O.point_add(O.point_mul(two, add), b)      # 2(a + b) + b
+        two_sub_plus = O.point_add(O.point_mul(two, sub), b)      # 2(a - b) + b
         for op, want in [(0, add), (1, sub), (2, add), (3, sub), (4, dbl), (5, four_plus), (6, add), (7, sub),
-                         (8, add), (9, add), (10, sub), (11, add), (12, sub)]:
+                         (8, add), (9, add), (10, sub), (11, add), (12, sub), (13, two_add_plus), (14, two_sub_plus)]:
             assert sim.sim_pt_op(op, wa, wb, r) == 0
             assert bytes(r) == want, (op, i)
 
