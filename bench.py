@@ -518,7 +518,10 @@ def bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropie
     import torch
     import time as _t
     batch = a.batch or 8 * threads
-    proofs = prep.prove_batch(b"bench", entropies(777), threads)[:batch]
+    # the proofs are made before timing on 4 threads: a consumer keeps its
+    # prover workspace (four proofs' buffers and MSM scratch, ~12 GB) for
+    # later batches, and the verifying threads need HBM of their own
+    proofs = prep.prove_batch(b"bench", entropies(777), min(threads, 4))[:batch]
     while len(proofs) < batch:
         proofs += proofs[:batch - len(proofs)]
     V = _commitments(ctx, syn)

@@ -2168,24 +2168,10 @@ DEVI void foldn_get(gec &c, const uint32_t *tb) {
 #ifndef FOLD3_PREFETCH
 #define FOLD3_PREFETCH 1   // the next op's table entry is loaded before the doublings
 #endif
+// the lane's odd multiples P, 3P, .. of the seven points into the block's
+// word-major table
 template <class P>
-__global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *__restrict__ Ap) {
-    const FoldNArgs &A = *Ap;
-    uint32_t b = blockIdx.x, sg = 0;
-    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
-    const uint32_t i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
-    if (i >= A.end[sg]) return;
-    const uint32_t v = A.vec[sg], nops = A.nops[sg];
-    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
-    const uint16_t *ops = A.ops[sg];
-    const uint32_t hq = A.hq;
-    gec P0;
-    if (nops == 0) {
-        load_as_cached(P0, Pin + i);
-        gec_store(A.out[v] + i, P0);
-        return;
-    }
-    uint32_t *tb = A.tab + (size_t)b * FOLDN_TABW + threadIdx.x;
+DEVI void foldn_build(const P *Pin, uint32_t hq, uint32_t i, uint32_t *tb) {
     for (int t = 0; t < FOLDN_K; t++) {
         gec c1;
         load_as_cached(c1, Pin + (size_t)(t + 1) * hq + i);
@@ -2209,24 +2195,31 @@ __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *
             }
         }
     }
-    auto entry = [&](uint32_t op) { return tb + (((op >> 8) & 7) * FOLDN_MULT + ((op >> 11) & 7)) * 40 * 64; };
+}
+DEVI const uint32_t *foldn_entry(const uint32_t *tb, uint32_t op) {
+    return tb + (((op >> 8) & 7) * FOLDN_MULT + ((op >> 11) & 7)) * 40 * 64;
+}
+// The Straus chain over a built table, then + P_i, out as a cached point.
+template <class P>
+DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i, uint32_t v, const uint32_t *tb) {
+    const uint32_t nops = A.nops[sg];
+    const uint16_t *ops = A.ops[sg];
     ge acc;
     {
         const uint32_t op = fold2_op(ops, 0);
         gec c;
-        foldn_get(c, entry(op));
+        foldn_get(c, foldn_entry(tb, op));
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
 #if FOLD3_PREFETCH
     gec c;
-    if (nops > 1) foldn_get(c, entry(fold2_op(ops, 1)));
-    const uint32_t tail = A.tail[sg];
+    if (nops > 1) foldn_get(c, foldn_entry(tb, fold2_op(ops, 1)));
     for (uint32_t k = 1; k < nops; k++) {
         const uint32_t op = fold2_op(ops, k);
         const uint32_t g = op & 255;
         gec cn;
-        if (k + 1 < nops) foldn_get(cn, entry(fold2_op(ops, k + 1)));
+        if (k + 1 < nops) foldn_get(cn, foldn_entry(tb, fold2_op(ops, k + 1)));
         if (g) {
             for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
             ge_dbl_t<true>(acc, acc);
@@ -2248,21 +2241,46 @@ __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *
             ge_dbl_t<true>(acc, acc);
         }
         gec c;
-        foldn_get(c, entry(op));
+        foldn_get(c, foldn_entry(tb, op));
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
     }
-    const uint32_t tail = A.tail[sg];
 #endif
+    const uint32_t tail = A.tail[sg];
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
         ge_dbl_t<true>(acc, acc);
     }
+    gec P0;
     load_as_cached(P0, Pin + i);
     ge r;
     ge_add_c(r, acc, P0);
     gec out;
     ge_to_cached(out, r);
     gec_store(A.out[v] + i, out);
+}
+DEVI bool foldn_lane(const FoldNArgs &A, uint32_t &sg, uint32_t &i) {
+    const uint32_t b = blockIdx.x;
+    sg = 0;
+    for (uint32_t k = 1; k < A.nseg; k++) if (b >= A.blk0[k]) sg = k;
+    i = A.start[sg] + (b - A.blk0[sg]) * 64 + threadIdx.x;
+    return i < A.end[sg];
+}
+template <class P>
+__global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *__restrict__ Ap) {
+    const FoldNArgs &A = *Ap;
+    uint32_t sg, i;
+    if (!foldn_lane(A, sg, i)) return;
+    const uint32_t v = A.vec[sg];
+    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
+    if (A.nops[sg] == 0) {
+        gec P0;
+        load_as_cached(P0, Pin + i);
+        gec_store(A.out[v] + i, P0);
+        return;
+    }
+    uint32_t *tb = A.tab + (size_t)blockIdx.x * FOLDN_TABW + threadIdx.x;
+    foldn_build(Pin, A.hq, i, tb);
+    foldn_chain(A, sg, Pin, i, v, tb);
 }
 size_t ipp_fold3_table_bytes(uint32_t hq, uint32_t nrange) {
     // blocks: per vector and range, whole 64-lane blocks
