@@ -698,7 +698,10 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
     import torch
     from concurrent.futures import ThreadPoolExecutor
     threads = a.threads or max(2, min(64, job_cpus() // max(world, 1)))   # synthesis is host work: one per CPU
-    batch = a.batch or 2 * threads
+    # 8 statements per thread per step: every statement's latency (~0.5 s:
+    # synthesis, upload, the serial TranscriptRng chain, device work) is paid
+    # once per call as pipeline fill, so short batches understate the rate
+    batch = a.batch or 8 * threads
     texts = [W.config5(50000 + 100003 * rank + i) for i in range(batch * (a.steps + a.warmup))]
     q = bpg.Synth(*texts[0]).q
 
@@ -751,8 +754,8 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
               "prove_ms": round((t3 - t2) * 1e3, 1), "prove_phases_ms": bpg.last_timings()}
     n_st = batch * a.steps * world
     out = {
-        "metric": "R1CS prove constraints/sec end to end over distinct statements (c_prove: parse + synthesis + "
-                  "upload + prove) at %d MI355X" % world,
+        "metric": "R1CS prove constraints/sec end to end over distinct statements (prove.rs:37-82: parse + "
+                  "synthesis + upload + prove) at %d MI355X" % world,
         "value": round(n_st * q / dt, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32 (255-bit integer field/scalar arithmetic)",

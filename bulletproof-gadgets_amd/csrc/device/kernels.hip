@@ -934,12 +934,12 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
     int lgK = 0;
     while ((1u << lgK) < K) lgK++;
     const ge *A = segA + (size_t)row * nseg, *T = segT + (size_t)row * nseg;
-    ge sumA, run, acc, p;
-    ge_identity(sumA); ge_identity(run); ge_identity(acc);
+    // sum_s A_s is added at the end (three points live at most, not four)
+    ge run, acc, p;
+    ge_identity(run); ge_identity(acc);
     for (int k = (int)K - 1; k >= 0; k--) {
         uint32_t s = t * K + k;
         if (s >= nseg) continue;
-        ge_load(p, A + s); ge_add(sumA, sumA, p);
         ge_load(p, T + s); ge_add(run, run, p);
         ge_add(acc, acc, run);
     }
@@ -961,7 +961,11 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
     ge_sub(q, acc, run);
     ge_add(q, q, suf);
     ge_dbl_n(q, lgL);                      // L * (...)
-    ge_add(q, q, sumA);
+    for (uint32_t k = 0; k < K; k++) {     // + this thread's A_s
+        uint32_t s = t * K + k;
+        if (s >= nseg) break;
+        ge_load(p, A + s); ge_add(q, q, p);
+    }
     __syncthreads();
     ge_store(&sh[t], q);
     for (int w = 128; w >= 1; w >>= 1) {
@@ -1095,8 +1099,8 @@ __global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ blkB, c
 }
 
 // Window width: lg(points) - 3 (measured best, profiles/r01 MSM window
-// sweeps). With BPG_MSM_WINDOW_MODEL=1, another width in [4, 16] when a
-// GF(p)-multiply count of the job says it needs 3% fewer: W entries per point (7M Niels / 8M cached madd)
+// sweeps), or another width in [4, 16] when a GF(p)-multiply count of the
+// job says it needs 3% fewer: W entries per point (7M Niels / 8M cached madd)
 // against 2 nmsm W 2^(c-1) bucket additions (9M each). Widths above 16 would
 // add a third sort pass. E.g. the IPP's 2^19-point jobs of rounds 2-4 take
 // c = 15 (17 windows of 16384 buckets) instead of 16 (16 of 32768).
@@ -1111,10 +1115,12 @@ static int msm_window(uint64_t total, int nmsm, int fmt) {
         const double W = (254 + w - 1) / w;
         return W * (double)total * madd + 2.0 * nmsm * W * (double)(1u << (w - 1)) * 9.0;
     };
-    // off by default: 74.0 / 74.6 vs 74.4 / 75.0 M constraints/s without it
-    // (profiles/r03d_ab_window_model_threads.txt) — the chip is VALU-bound,
-    // the extra window's additions cost more than the smaller bucket rows save
-    static const bool model = [] { const char *e = getenv("BPG_MSM_WINDOW_MODEL"); return e && e[0] == '1'; }();
+    // On by default since jobs hold four proofs' MSMs (nmsm = 8 for the IPP
+    // rounds, so the bucket term weighs 4x more): 82.7 / 83.1 vs 81.6 / 82.0 M
+    // constraints/s without it (profiles/r03o_ab_rowreduce_window_model.txt);
+    // at one proof per job it was neutral (74.0 / 74.6 vs 74.4 / 75.0 M,
+    // r03d_ab_window_model_threads.txt). BPG_MSM_WINDOW_MODEL=0: lg - 3 only.
+    static const bool model = [] { const char *e = getenv("BPG_MSM_WINDOW_MODEL"); return !(e && e[0] == '0'); }();
     int best = c;
     for (int w = 4; w <= 16; w++)
         if (cost(w) < cost(best)) best = w;
