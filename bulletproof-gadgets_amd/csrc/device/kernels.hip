@@ -37,6 +37,27 @@ static_assert(sizeof(NielsD) == sizeof(gen) && sizeof(gen) == 128, "niels layout
 
 static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
+// Wave priorities (s_setprio, 0-3; 0 = the hardware default). Under the
+// bench's concurrency a latency-bound kernel (window-row reduction, run
+// merges, final run sums) runs ~10x its isolated time because the SIMDs'
+// issue arbiter serves the VALU-bound waves of other streams first, and it
+// holds its registers (225 VGPRs per row-reduction wave) all that time.
+// Raising its waves' priority lets it issue whenever it is ready and leave
+// sooner; the VALU-bound kernels lose no work, only the order of issue.
+//   BPG_LAT_PRIO:  row reduction, bucket segments, run merges, final run sums
+//   BPG_SORT_PRIO: digit extraction and the radix-sort kernels
+//   BPG_FOLD_PRIO: the Straus triple fold (one wave per SIMD, 332 VGPRs)
+#ifndef BPG_LAT_PRIO
+#define BPG_LAT_PRIO 0
+#endif
+#ifndef BPG_SORT_PRIO
+#define BPG_SORT_PRIO 0
+#endif
+#ifndef BPG_FOLD_PRIO
+#define BPG_FOLD_PRIO 0
+#endif
+#define WAVE_PRIO(p) do { if constexpr ((p) > 0) __builtin_amdgcn_s_setprio((p)); } while (0)
+
 static thread_local ProfSink *tl_sink = nullptr;
 void set_prof_sink(ProfSink *s) { tl_sink = s; }
 void event_wait(hipEvent_t ev) {
@@ -247,6 +268,7 @@ struct TileGeo {
 };
 __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G) {
+    WAVE_PRIO(BPG_SORT_PRIO);
     __shared__ uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -336,6 +358,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ tiles, uint32_t nb,
                                                       uint32_t *__restrict__ hist) {
     constexpr uint32_t RS_BINS = 1u << RS_BITS;
+    WAVE_PRIO(BPG_SORT_PRIO);
     __shared__ uint32_t h[RS_BINS];
     if (threadIdx.x < RS_BINS) h[threadIdx.x] = 0;
     __syncthreads();
@@ -349,6 +372,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict
 __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ total) {
     __shared__ uint32_t sm[256];
+    WAVE_PRIO(BPG_SORT_PRIO);
     const uint32_t t = threadIdx.x;
     uint32_t *h = hist + (size_t)blockIdx.x * nb;
     uint32_t carry = 0;
@@ -384,6 +408,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
                                                          const uint32_t *__restrict__ total,
                                                          uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
     constexpr uint32_t RS_BINS = 1u << RS_BITS;
+    WAVE_PRIO(BPG_SORT_PRIO);
     __shared__ uint32_t base[RS_BINS], lstart[RS_BINS], tot[RS_BINS];
     __shared__ uint32_t cnt[STABLE ? RS_ROUNDS : 1][RS_BLOCK / 64][RS_BINS];   // ballot ranking only
     __shared__ uint32_t lk[RS_ITER], lv[RS_ITER];
@@ -712,6 +737,7 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
                                                         ge *__restrict__ pout, ge *__restrict__ buckets,
                                                         uint8_t *__restrict__ bflag) {
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
+    if constexpr (!FIRST) WAVE_PRIO(BPG_LAT_PRIO);
     __shared__ uint32_t sv[FIRST ? RBK_CHUNK + RBK_BLOCK : 1];
     __shared__ uint64_t sptr[FIRST ? 2 * MSM_MAXSEG : 1];
     const uint32_t t = threadIdx.x;
@@ -864,6 +890,7 @@ __global__ __launch_bounds__(64, BPG_LAT_WAVES) void k_rbk_final(const uint32_t 
                                                   uint64_t E, uint32_t invalid, int cw, ge *__restrict__ buckets,
                                                   uint8_t *__restrict__ bflag) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    WAVE_PRIO(BPG_LAT_PRIO);
     if (i >= E) return;
     const uint32_t k = RBK_KEY(keys[i]);
     if (k == invalid || (i > 0 && RBK_KEY(keys[i - 1]) == k)) return;
@@ -899,6 +926,7 @@ DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict
 __global__ __launch_bounds__(64, BSEG_WAVES) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
                                                    uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
                                                    ge *__restrict__ segA, ge *__restrict__ segT) {
+    WAVE_PRIO(BPG_LAT_PRIO);
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= rows * nseg) return;
     uint32_t row = t / nseg, sgi = t % nseg;
@@ -930,6 +958,7 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
                                                     ge *__restrict__ rows_out) {
     __shared__ ge sh[256];
     const uint32_t row = blockIdx.x, t = threadIdx.x;
+    WAVE_PRIO(BPG_LAT_PRIO);
     const uint32_t K = (nseg + 255) / 256;
     int lgK = 0;
     while ((1u << lgK) < K) lgK++;
@@ -2273,6 +2302,7 @@ DEVI bool foldn_lane(const FoldNArgs &A, uint32_t &sg, uint32_t &i) {
 }
 template <class P>
 __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *__restrict__ Ap) {
+    WAVE_PRIO(BPG_FOLD_PRIO);
     const FoldNArgs &A = *Ap;
     uint32_t sg, i;
     if (!foldn_lane(A, sg, i)) return;
