@@ -54,6 +54,8 @@ def parse():
                          "one HIP stream each, four proofs at a time, at most 24 proofs in flight at 2^20 "
                          "(default 16 with >= 4 cpus; verify mode 24)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fold-tables", type=int, default=-1, choices=(-1, 0, 1),
+                    help="IPP comb tables: 1 on, 0 off (the path a device without ~208 GB free takes), -1 default")
     ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification); latency: one proof at a time, sharded over all "
@@ -349,6 +351,8 @@ def main():
     bpg.set_seed(1000 + srank)
     syn = bpg.Synth(inst, wit, gad)
     ctx = bpg.Context(dev)
+    if a.fold_tables >= 0:
+        ctx.set_strategy(fold_tables=a.fold_tables)
     if a.mode == "latency":
         return bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W)
     # cold setup, outside the timed region: BulletproofGens::new (prove.rs:78,
@@ -490,7 +494,8 @@ def main():
         "config": {"workload": W.NAMES[a.config], "n_gates": n, "N": N, "q_constraints": q,
                    "proofs_per_step_per_gpu": batch, "host_threads_per_gpu": threads,
                    "parallelism": "independent proofs per GPU (%d ranks)" % world,
-                   "pipeline": "the K steps' proofs stream through one producer/consumer pipeline"},
+                   "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
+                   "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables]},
         "host_cores_busy": round(host_busy, 2),
         "hbm_used_gb": round((total_b - free_b) / 1e9, 1),
         "latency_ms_single_proof": round(single_ms, 1),

@@ -41,17 +41,22 @@ static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t -
 // bench's concurrency a latency-bound kernel (window-row reduction, run
 // merges, final run sums) runs ~10x its isolated time because the SIMDs'
 // issue arbiter serves the VALU-bound waves of other streams first, and it
-// holds its registers (225 VGPRs per row-reduction wave) all that time.
-// Raising its waves' priority lets it issue whenever it is ready and leave
-// sooner; the VALU-bound kernels lose no work, only the order of issue.
+// holds its registers (225 VGPRs per row-reduction wave) and LDS all that
+// time; the memory-bound sort kernels likewise. Raising their waves'
+// priority lets them issue whenever they are ready and leave sooner; the
+// VALU-bound kernels lose no work, only the order of issue.
 //   BPG_LAT_PRIO:  row reduction, bucket segments, run merges, final run sums
 //   BPG_SORT_PRIO: digit extraction and the radix-sort kernels
 //   BPG_FOLD_PRIO: the Straus triple fold (one wave per SIMD, 332 VGPRs)
+// Default 2 / 3 / 0: 84.45 / 84.39 vs 83.91 / 83.56 M constraints/s
+// (profiles/r03r_ab_priority_stop.txt; tail 2 + sort 1: 84.14 / 84.09, sort
+// 1 alone 83.99 / 83.84; the fold at 1 gave nothing more,
+// r03q_ab_wave_priority.txt).
 #ifndef BPG_LAT_PRIO
-#define BPG_LAT_PRIO 0
+#define BPG_LAT_PRIO 2
 #endif
 #ifndef BPG_SORT_PRIO
-#define BPG_SORT_PRIO 0
+#define BPG_SORT_PRIO 3
 #endif
 #ifndef BPG_FOLD_PRIO
 #define BPG_FOLD_PRIO 0
@@ -1411,6 +1416,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         E = 2 * (uint64_t)nblocks * RBK_BLOCK;
         kin = kout;
         pin = pout;
+        // (handing the runs to the final sums after two passes once <= 2^18
+        // slots remain measured 0.4% slower: profiles/r03r_ab_priority_stop.txt)
         if (E <= 8192 || p.passes >= 5) break;
         const bool a = kout == (uint32_t *)rk_a_.p;
         kout = a ? (uint32_t *)rk_b_.p : (uint32_t *)rk_a_.p;
