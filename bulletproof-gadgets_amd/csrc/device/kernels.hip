@@ -61,6 +61,23 @@ static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t -
 #ifndef BPG_FOLD_PRIO
 #define BPG_FOLD_PRIO 0
 #endif
+//   BPG_MISC_PRIO: the scalar-vector kernels between a proof's MSM jobs (IPP
+//   round preparation and scalar folds, flatten, t(x), powers, draws)
+//   BPG_CACHED_PRIO: MSM pass 1 over folded (cached) bases
+//   BPG_COMB_PRIO: the comb-table fold (rounds 0-1)
+// MSM pass 1 over the generators, the bulk of the VALU work, stays at 0: the
+// throughput filler under everything on a proof's critical path. Misc 2 and
+// cached 1 on top of tail 2 / sort 3: 85.28 / 85.21 vs 84.54 / 84.56 M
+// (profiles/r03s_ab_priority.txt; misc 2 alone 85.14 / 84.72).
+#ifndef BPG_MISC_PRIO
+#define BPG_MISC_PRIO 2
+#endif
+#ifndef BPG_CACHED_PRIO
+#define BPG_CACHED_PRIO 1
+#endif
+#ifndef BPG_COMB_PRIO
+#define BPG_COMB_PRIO 0
+#endif
 #define WAVE_PRIO(p) do { if constexpr ((p) > 0) __builtin_amdgcn_s_setprio((p)); } while (0)
 
 static thread_local ProfSink *tl_sink = nullptr;
@@ -743,6 +760,7 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
                                                         uint8_t *__restrict__ bflag) {
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
     if constexpr (!FIRST) WAVE_PRIO(BPG_LAT_PRIO);
+    if constexpr (FIRST && FMT == MSM_CACHED) WAVE_PRIO(BPG_CACHED_PRIO);
     __shared__ uint32_t sv[FIRST ? RBK_CHUNK + RBK_BLOCK : 1];
     __shared__ uint64_t sptr[FIRST ? 2 * MSM_MAXSEG : 1];
     const uint32_t t = threadIdx.x;
@@ -1470,6 +1488,7 @@ DEVI sc sc_one_raw() { sc o; sc_zero(o); o.v[0] = 1; return o; }
 // only its own lanes).
 __global__ void k_wide_reduce(const uint32_t *__restrict__ wide, uint32_t count, uint32_t stride, uint32_t offset,
                               sc *__restrict__ out) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const uint4 *w = reinterpret_cast<const uint4 *>(wide + 16 * ((size_t)i * stride + offset));
@@ -1494,6 +1513,7 @@ void launch_wide_reduce(const uint8_t *wide, uint32_t count, uint32_t stride, ui
 
 // out[i] = mont(base^(start+i)); base2[b] = mont(base^(2^b))
 __global__ void k_pow_table(const sc *__restrict__ base2, uint64_t start, uint32_t count, sc *__restrict__ out) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     uint64_t e = start + i;
@@ -1513,6 +1533,7 @@ void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out
 }
 __global__ void k_pow_expand(const sc *__restrict__ lo, const sc *__restrict__ hi, uint32_t count, sc mult,
                              sc *__restrict__ out) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     sc a, b, r;
@@ -1538,6 +1559,7 @@ DEVI void flat_term(sc &acc, uint32_t q, const sc &coeff, const sc *zlo, const s
     sc_add(acc, acc, t);
 }
 __global__ void k_flatten_short(CscDev c, const sc *__restrict__ zlo, const sc *__restrict__ zhi, sc *__restrict__ out) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= c.nshort) return;
     uint32_t col = c.short_cols[t];
@@ -1551,6 +1573,7 @@ __global__ void k_flatten_short(CscDev c, const sc *__restrict__ zlo, const sc *
 }
 __global__ __launch_bounds__(64) void k_flatten_long(CscDev c, const sc *__restrict__ zlo, const sc *__restrict__ zhi,
                                                      sc *__restrict__ out) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     __shared__ sc sh[64];
     uint32_t t = blockIdx.x, lane = threadIdx.x;
     if (t >= c.nlong) return;
@@ -1583,6 +1606,7 @@ __global__ void k_lr_build(const sc *__restrict__ aL, const sc *__restrict__ aR,
                            const sc *__restrict__ wL, const sc *__restrict__ wR, const sc *__restrict__ wO,
                            const sc *__restrict__ ypm, const sc *__restrict__ yipm, uint32_t n, sc *__restrict__ l1,
                            sc *__restrict__ r0, sc *__restrict__ r1, sc *__restrict__ r3) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     sc a, b, y, t, u;
@@ -1624,6 +1648,7 @@ __global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const 
                                                const sc *__restrict__ l3, const sc *__restrict__ r0,
                                                const sc *__restrict__ r1, const sc *__restrict__ r3, uint32_t n,
                                                sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[6];
     for (int k = 0; k < 6; k++) sc_zero(acc[k]);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1642,6 +1667,7 @@ __global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const 
 // out[k] = R * sum_b partial[b*K + k]   (one block per k)
 __global__ __launch_bounds__(256) void k_reduce_cols(const sc *__restrict__ partial, uint32_t nb, uint32_t K,
                                                      sc *__restrict__ out, uint32_t out_stride, int mode) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     __shared__ sc sh[256];
     uint32_t k = blockIdx.x, tid = threadIdx.x;
     sc acc; sc_zero(acc);
@@ -1674,6 +1700,7 @@ void launch_tpoly(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, co
 __global__ __launch_bounds__(256) void k_flatten_range(const sc *__restrict__ coeff, const uint32_t *__restrict__ row,
                                                        uint32_t k0, uint32_t k1, const sc *__restrict__ zlo,
                                                        const sc *__restrict__ zhi, sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[1];
     sc_zero(acc[0]);
     for (uint32_t k = k0 + blockIdx.x * blockDim.x + threadIdx.x; k < k1; k += gridDim.x * blockDim.x) {
@@ -1693,6 +1720,7 @@ void launch_flatten_huge(const CscDev &csc, uint32_t col, uint32_t k0, uint32_t 
 }
 __global__ __launch_bounds__(256) void k_dot(const sc *__restrict__ a, const sc *__restrict__ b, uint32_t n,
                                              sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[1];
     sc_zero(acc[0]);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1714,6 +1742,7 @@ __global__ void k_lr_eval(const sc *__restrict__ l1, const sc *__restrict__ l2, 
                           const sc *__restrict__ r0, const sc *__restrict__ r1, const sc *__restrict__ r3,
                           const sc *__restrict__ ypm, uint32_t n, uint32_t N, sc xm, sc x2m, sc *__restrict__ a,
                           sc *__restrict__ b) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     sc ra, rb;
@@ -1746,6 +1775,7 @@ void launch_lr_eval(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, 
 __global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, const sc *__restrict__ b,
                                                   const sc *__restrict__ yipm, IppRoundArgs A, sc *__restrict__ out,
                                                   sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
     const uint32_t h = A.h;
@@ -1777,6 +1807,7 @@ void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundA
 }
 // u, uinv in Montgomery form
 __global__ void k_ipp_fold_scalars(sc *__restrict__ a, sc *__restrict__ b, uint32_t h, sc um, sc uim) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= h) return;
     sc x, y, t1, t2;
@@ -2494,6 +2525,7 @@ void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab
 // with per-lane-range coefficient digits (signed radix 2^COMB_BITS, LSB
 // first); no doublings: every nonzero digit is one table read and one 7M madd.
 __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restrict__ Ap) {
+    WAVE_PRIO(BPG_COMB_PRIO);
     const CombArgs &A = *Ap;
     const uint32_t nb = (A.h1 + 63) / 64;
     const uint32_t v = blockIdx.x >= nb ? 1 : 0;
@@ -2575,6 +2607,7 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
 __global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a, const sc *__restrict__ b,
                                                        const sc *__restrict__ yipm, IppRoundArgs A, LazyArgs Z,
                                                        sc *__restrict__ out, sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
     const uint32_t h = A.h, h0 = Z.h0, n = A.n;
@@ -2624,6 +2657,7 @@ void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppR
 __global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a, const sc *__restrict__ b,
                                                         const sc *__restrict__ yipm, IppRoundArgs A, Deep2Args Z,
                                                         sc *__restrict__ out, sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
     const uint32_t h = A.h, n = A.n;
@@ -2677,6 +2711,7 @@ __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a,
                                                        const sc *__restrict__ yipm, IppRoundArgs A, uint32_t M,
                                                        const sc *__restrict__ wG, const sc *__restrict__ wH,
                                                        sc *__restrict__ out, sc *__restrict__ partial) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
     const uint32_t h = A.h, n = A.n;
@@ -2725,6 +2760,7 @@ void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppR
 }
 __global__ void k_ipp_tail_weights(sc *__restrict__ wG, sc *__restrict__ wH, uint32_t M, uint32_t h, uint32_t n,
                                    sc rGa, sc rGb, sc rHa, sc rHb) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= M) return;
     const uint32_t i = j % (2 * h);
@@ -2744,6 +2780,7 @@ void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t 
 }
 
 __global__ void k_fill_scalars(sc *dst, sc val, uint32_t count) {
+    WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) sc_store(dst + i, val);
 }
