@@ -2,7 +2,9 @@
 # End-of-round check B: the default bench command under rocprofv3
 # --kernel-trace --stats (kernel table + occupancy timeline; the bench's own
 # HIP-event bracketing on), the PMC passes of the current build (one counter
-# group per pass, kernel trace only), then the secondary modes.
+# group per pass, kernel trace only), then the secondary modes, then the
+# --gpus launcher on hardware: two self-spawned ranks sharing the one GPU
+# over gloo (RCCL refuses two ranks on one device), config 4.
 set -o pipefail
 mkdir -p gpurun_out
 R=${R:-r03z}
@@ -18,4 +20,5 @@ timeout -k 10 300 python bench.py --mode verify --steps 3 --warmup 1 > gpurun_ou
 timeout -k 10 300 python bench.py --mode verify-sharded --steps 20 --warmup 3 > gpurun_out/${R}_verify_sharded.json 2> gpurun_out/${R}_verify_sharded.err || exit $?
 timeout -k 10 300 python bench.py --mode latency --steps 5 --warmup 1 > gpurun_out/${R}_latency.json 2> gpurun_out/${R}_latency.err || exit $?
 timeout -k 10 600 python bench.py --mode statements --steps 2 --warmup 1 > gpurun_out/${R}_statements.json 2> gpurun_out/${R}_statements.err || exit $?
+BENCH_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --config 4 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${R}_bench_2ranks_shared_gpu.json 2> gpurun_out/${R}_bench_2ranks.err || exit $?
 echo done
