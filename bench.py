@@ -50,9 +50,13 @@ def parse():
     ap.add_argument("--config", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0, help="proofs per step (default: 24 x threads)")
     ap.add_argument("--threads", type=int, default=0,
-                    help="host threads per GPU: half draw the TranscriptRng streams (at most 8), the rest drive "
-                         "one HIP stream each, four proofs at a time, at most 24 proofs in flight at 2^20 "
-                         "(default 16 with >= 4 cpus; verify mode 24)")
+                    help="host threads per GPU: the TranscriptRng producers plus the device consumers (one HIP "
+                         "stream each, four proofs at a time, admitted by HBM: at most 24 proofs in flight at 2^20). "
+                         "Default: producers + 8 (verify mode 24)")
+    ap.add_argument("--producers", type=int, default=0,
+                    help="TranscriptRng producer threads per GPU (default: one per CPU of the rank's share, at most 8)")
+    ap.add_argument("--cpus", type=int, default=0,
+                    help="pin this rank to its first N CPUs (emulates the per-rank CPU share of a multi-GPU node)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fold-tables", type=int, default=-1, choices=(-1, 0, 1),
                     help="IPP comb tables: 1 on, 0 off (the path a device without ~208 GB free takes), -1 default")
@@ -302,6 +306,9 @@ def main():
         print(json.dumps({"rank": rank, "world": world, "local": local, "master": os.environ.get("MASTER_ADDR"),
                           "spawned": os.environ.get("BENCH_SPAWNED") == "1"}), flush=True)
         return
+    if a.cpus:   # before anything starts a thread: the pool inherits the mask
+        cpus = sorted(os.sched_getaffinity(0))[:a.cpus]
+        os.sched_setaffinity(0, cpus)
     if rank == 0:
         heartbeat()
     import torch
@@ -326,20 +333,22 @@ def main():
     global DIST_INFO
     DIST_INFO = dist_info(torch, dist, D, dev, world)
     ncpu = job_cpus()
-    # consumers mostly sleep on the device (event polls), so 16 threads keep
-    # ~3 host cores busy: 8 RNG producers + 6 device streams, each proving
-    # four proofs at once (bpg_prove_batch's default lockstep; its in-flight
-    # cap for HBM leaves the other 2 threads unused at 2^20)
-    per_rank = ncpu // max(world, 1) if world > 1 else ncpu
-    # (host_cores_busy ~3.2 at 16 threads, so a rank may run 4 threads per CPU of its share)
-    threads = a.threads or max(1, min(16, per_rank * 4))
+    # the rank's CPU share: the job's CPUs (cgroup quota, else affinity)
+    # divided among the ranks on this node
+    per_rank = max(1, ncpu // max(world, 1)) if world > 1 else ncpu
+    # producers draw the TranscriptRng streams (one keeps a core busy, ~20
+    # proofs/s at 2^20): one per CPU of the rank's share, at most 8. Consumers
+    # mostly sleep on the device (event polls); the library admits them by HBM
+    # (six streams of four proofs at 2^20 next to the comb tables)
+    producers = a.producers or max(1, min(8, per_rank))
+    threads = a.threads or producers + 8
     if a.mode == "verify" and not a.threads:
         threads = max(1, min(24, per_rank * 3 // 2))   # one HIP stream per verifying thread
     threads = min(threads, 64)
-    # 384 proofs per step (24 per host thread at the default 16); the timed
-    # steps run as one continuous pipeline (below), so the end-of-batch drain
-    # is paid once
-    batch = a.batch or 24 * threads
+    # 384 proofs per step at the default layout (24 per host thread at 16
+    # threads); the timed steps run as one continuous pipeline (below), so the
+    # end-of-batch drain is paid once
+    batch = a.batch or 384
 
     if a.mode == "statements":
         return bench_statements(a, bpg, dist, D, rank, world, W)
@@ -353,6 +362,7 @@ def main():
     ctx = bpg.Context(dev)
     if a.fold_tables >= 0:
         ctx.set_strategy(fold_tables=a.fold_tables)
+    ctx.set_pipeline(producers=min(producers, 8))
     if a.mode == "latency":
         return bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W)
     # cold setup, outside the timed region: BulletproofGens::new (prove.rs:78,
@@ -395,6 +405,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     c1 = os.times()
+    pipe = bpg.last_batch_stats()
     host_busy = ((c1.user - c0.user) + (c1.system - c0.system)) / dt   # host cores kept busy by this rank
     if os.environ.get("BENCH_THREAD_CPU"):   # diagnostic: per-thread CPU seconds (utime, stime)
         rows = []
@@ -497,6 +508,10 @@ def main():
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
                    "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables]},
         "host_cores_busy": round(host_busy, 2),
+        # the producer/consumer pipeline of the timed batch (bpg_last_batch_stats):
+        # consumer time starved of ready proofs while producers were drawing
+        # (after the pipeline fill) and host_bound when that exceeds a tenth
+        "pipeline": pipeline_line(pipe, ncpu, per_rank, a.cpus, a.steps * batch),
         "hbm_used_gb": round((total_b - free_b) / 1e9, 1),
         "latency_ms_single_proof": round(single_ms, 1),
         "cold_setup_ms": round(prepare_ms, 1),
@@ -513,6 +528,26 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pipeline_line(p, ncpu, per_rank, pinned, nproofs):
+    span = max(1e-9, (p["wall_ms"] - p["fill_ms"]) * p["consumers"])
+    return {"producers": p["producers"], "consumers": p["consumers"], "proofs_per_consumer_step": p["lockstep"],
+            "proofs_in_flight": p["inflight"], "host_bound": p["host_bound"],
+            "consumer_starved_frac": round(p["consumer_starved_ms"] / span, 4),
+            "consumer_starved_ms": round(p["consumer_starved_ms"], 1), "fill_ms": round(p["fill_ms"], 1),
+            "producer_slot_wait_frac": round(p["producer_slot_wait_ms"] / max(1e-9, p["wall_ms"] * p["producers"]), 4),
+            "producer_draw_ms": round(p["producer_draw_ms"], 1),
+            # proofs one producer draws per second of its busy time, and what
+            # all producers could draw against what the device consumed
+            "proofs_per_busy_s_per_producer": round(nproofs / (p["producer_draw_ms"] / 1e3), 2)
+            if p["producer_draw_ms"] else None,
+            "producer_capacity_proofs_per_s": round(p["producers"] * nproofs / (p["producer_draw_ms"] / 1e3), 1)
+            if p["producer_draw_ms"] else None,
+            "proofs_per_s": round(nproofs / (p["wall_ms"] / 1e3), 2),
+            "consumers_by_threads": p["consumers_by_threads"], "consumers_by_hbm": p["consumers_by_hbm"],
+            "est_gb_per_consumer": round(p["est_gb_per_consumer"], 2), "hbm_free_gb_at_start": round(p["hbm_free_gb"], 1),
+            "cpus": {"job": ncpu, "rank_share": per_rank, "process": p["process_cpus"], "pinned": pinned or None}}
 
 
 def bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropies, q, n, N, W):
@@ -730,6 +765,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         # here, while the HIP runtime is certainly still up
         pool.shutdown(wait=True)
         api = "c_prove on %d threads" % threads
+        stages = None
     else:   # bpg_prove_statements: lockstep RNG over distinct statements, device consumers
         bpg.prove_statements("bench", texts[:batch * a.warmup], threads)
         barrier()
@@ -737,6 +773,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         outs = bpg.prove_statements("bench", texts[batch * a.warmup:], threads)
         barrier()
         dt = time.perf_counter() - t0
+        stages = bpg.last_statements_stats()
         if any(o is None for o in outs):
             raise SystemExit("bench: a statement failed: %s" % bpg.last_error())
         api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(16, max(1, threads // 2)))
@@ -768,6 +805,9 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         "config": {"workload": W.NAMES[5], "q_constraints": q, "statements_per_step_per_gpu": batch,
                    "host_threads_per_gpu": threads, "api": api},
         "statements_per_s": round(n_st / dt, 2),
+        # bpg_last_statements_stats: busy / idle ms per stage summed over
+        # threads, and the stage that bounded the call
+        "stages": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in stages.items()} if stages else None,
         "single_statement_ms": phases,
         "dist": DIST_INFO,
     }

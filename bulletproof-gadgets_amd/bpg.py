@@ -32,6 +32,7 @@ EXPORTS = [
     "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
     "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim", "bpg_prove_statements",
+    "bpg_ctx_set_pipeline", "bpg_last_batch_stats", "bpg_last_statements_stats",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -93,6 +94,9 @@ def lib():
         L.bpg_ctx_set_fold_pairs.argtypes = [vp, ctypes.c_int]
         L.bpg_ctx_set_ipp_tail.argtypes = [vp, ctypes.c_int]
         L.bpg_ctx_setup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.bpg_ctx_set_pipeline.argtypes = [vp, u32, u32, u32]
+        L.bpg_last_batch_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.bpg_last_statements_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_r1cs_prove_sharded.argtypes = [vp, vp, sz, vp, vp, u32, u32, ALLGATHER_FN, vp, vp, sz,
                                              ctypes.POINTER(sz), vp]
         L.bpg_prepare.restype = vp
@@ -369,6 +373,12 @@ class Context:
                 lib().bpg_ctx_set_ipp_tail(self.h, ipp_tail) != 0:
             raise BpgError("bad strategy")
 
+    def set_pipeline(self, producers=0, lockstep=0, max_inflight=0):
+        """bpg_ctx_set_pipeline: layout of prove_batch on circuits prepared
+        through this context afterwards (0 = automatic)."""
+        if lib().bpg_ctx_set_pipeline(self.h, producers, lockstep, max_inflight) != 0:
+            raise BpgError("bad pipeline layout")
+
     def setup_stats(self):
         arr = (ctypes.c_double * 5)()
         lib().bpg_ctx_setup_stats(self.h, arr, 5)
@@ -553,3 +563,37 @@ def last_timings():
     arr = (ctypes.c_double * 5)()
     lib().bpg_last_timings(arr, 5)
     return {"rng_ms": arr[0], "commit_ms": arr[1], "vec_ms": arr[2], "ipp_ms": arr[3], "total_ms": arr[4]}
+
+
+BATCH_STATS = ("producers", "consumers", "lockstep", "inflight", "wall_ms", "fill_ms", "consumer_starved_ms",
+               "producer_slot_wait_ms", "producer_draw_ms", "consumer_prove_ms", "host_bound", "hbm_free_gb",
+               "est_gb_per_consumer", "consumers_by_threads", "consumers_by_hbm", "process_cpus")
+
+
+def last_batch_stats():
+    """bpg_last_batch_stats: the last prove_batch's layout and pipeline counters."""
+    arr = (ctypes.c_double * len(BATCH_STATS))()
+    lib().bpg_last_batch_stats(arr, len(BATCH_STATS))
+    d = dict(zip(BATCH_STATS, arr))
+    d["host_bound"] = bool(d["host_bound"])
+    for k in ("producers", "consumers", "lockstep", "inflight", "consumers_by_threads", "consumers_by_hbm",
+              "process_cpus"):
+        d[k] = int(d[k])
+    return d
+
+
+STATEMENTS_STATS = ("workers", "consumers", "limit", "wall_ms", "synth_ms", "prepare_ms", "rng_ms", "prove_ms",
+                    "worker_idle_ms", "consumer_idle_ms", "bound_stage", "hbm_limit", "est_gb_per_statement")
+
+
+def last_statements_stats():
+    """bpg_last_statements_stats: per-stage busy / idle time of the last
+    prove_statements call and the stage that bounded it."""
+    arr = (ctypes.c_double * len(STATEMENTS_STATS))()
+    lib().bpg_last_statements_stats(arr, len(STATEMENTS_STATS))
+    d = dict(zip(STATEMENTS_STATS, arr))
+    d["bound_stage"] = {0: "none", 1: "cpu workers (synthesis + prepare + rng)", 2: "device consumers"}.get(
+        int(d["bound_stage"]), "?")
+    for k in ("workers", "consumers", "limit", "hbm_limit"):
+        d[k] = int(d[k])
+    return d

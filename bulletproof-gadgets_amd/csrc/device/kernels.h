@@ -104,6 +104,11 @@ class MsmEngine {
     // Returns the plan (window width c and count W are needed by the host
     // combine). Segments: at most MSM_MAX_SEGS, all bases in format `fmt`.
     MsmPlan enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_host, int fmt, PtD *rows_direct = nullptr);
+    // device bytes the engine holds now
+    size_t bytes() const;
+    // device bytes the scratch of a job of `total` points in `nmsm` MSMs grows
+    // to (what enqueue reserves; HBM admission of the batched prover)
+    static size_t job_bytes(uint64_t total, int nmsm, int fmt);
   private:
     void reserve(const MsmPlan &p);
     hipStream_t st_;

@@ -52,15 +52,9 @@ static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t -
 // (profiles/r03r_ab_priority_stop.txt; tail 2 + sort 1: 84.14 / 84.09, sort
 // 1 alone 83.99 / 83.84; the fold at 1 gave nothing more,
 // r03q_ab_wave_priority.txt).
-#ifndef BPG_LAT_PRIO
-#define BPG_LAT_PRIO 2
-#endif
-#ifndef BPG_SORT_PRIO
-#define BPG_SORT_PRIO 3
-#endif
-#ifndef BPG_FOLD_PRIO
-#define BPG_FOLD_PRIO 0
-#endif
+static constexpr int BPG_LAT_PRIO = 2;
+static constexpr int BPG_SORT_PRIO = 3;
+static constexpr int BPG_FOLD_PRIO = 0;
 //   BPG_MISC_PRIO: the scalar-vector kernels between a proof's MSM jobs (IPP
 //   round preparation and scalar folds, flatten, t(x), powers, draws)
 //   BPG_CACHED_PRIO: MSM pass 1 over folded (cached) bases
@@ -69,22 +63,15 @@ static inline unsigned nblk(uint64_t n, unsigned t) { return (unsigned)((n + t -
 // throughput filler under everything on a proof's critical path. Misc 2 and
 // cached 1 on top of tail 2 / sort 3: 85.28 / 85.21 vs 84.54 / 84.56 M
 // (profiles/r03s_ab_priority.txt; misc 2 alone 85.14 / 84.72).
-#ifndef BPG_MISC_PRIO
-#define BPG_MISC_PRIO 2
-#endif
-#ifndef BPG_CACHED_PRIO
-#define BPG_CACHED_PRIO 1
-#endif
-#ifndef BPG_COMB_PRIO
-#define BPG_COMB_PRIO 0
-#endif
+static constexpr int BPG_MISC_PRIO = 2;
+static constexpr int BPG_CACHED_PRIO = 1;
+static constexpr int BPG_COMB_PRIO = 0;
 #define WAVE_PRIO(p) do { if constexpr ((p) > 0) __builtin_amdgcn_s_setprio((p)); } while (0)
 
 static thread_local ProfSink *tl_sink = nullptr;
 void set_prof_sink(ProfSink *s) { tl_sink = s; }
 void event_wait(hipEvent_t ev) {
-    static const long spin_us = [] { const char *e = getenv("BPG_WAIT_SLEEP_US"); return e ? atol(e) : 50L; }();
-    if (spin_us < 0) { BPG_HIP(hipEventSynchronize(ev)); return; }
+    const long spin_us = 50;
     for (;;) {
         const hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) return;
@@ -237,13 +224,9 @@ void launch_decompress(const uint32_t *in, NielsD *out, int *ok, uint32_t count,
 // buckets + a weighted correction, then a block reduction per row); the host
 // combines rows with c doublings each.
 // ===========================================================================
-#ifndef RBK_T
-#define RBK_T 16
-#endif
-#ifndef RBK_BLOCK
-#define RBK_BLOCK 256
-#endif
-#define RBK_CHUNK (RBK_T * RBK_BLOCK)
+static constexpr uint32_t RBK_T = 16;        // entries per thread chunk of the run reduction
+static constexpr uint32_t RBK_BLOCK = 256;
+static constexpr uint32_t RBK_CHUNK = RBK_T * RBK_BLOCK;
 #define MSM_MAXSEG MSM_MAX_SEGS
 struct SegTab {
     const sc *scal[MSM_MAXSEG];
@@ -357,19 +340,7 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
 // Stable ranking inside a wave: 7 ballots give each lane the mask of lanes
 // holding its digit; rank = popcount of that mask below the lane.
 // ---------------------------------------------------------------------------
-// RS_SEGSORT 1: two-digit sorts run the high digit tiled, then each (row, high
-// digit) segment by its low digit in one block (k_rs_segsort: no global
-// histogram, no stable ranking). Measured 67.8 vs 71.9 M constraints/s
-// (profiles/r02v_ab_segsort.txt): its entries land at scattered 4-byte
-// positions inside the segment, where the tiled scatter writes runs staged in
-// LDS. Off by default.
-#ifndef RS_SEGSORT
-#define RS_SEGSORT 0
-#endif
 // Digits are RS_BITS = 7 or 8 bits wide (8 when it saves a pass).
-#ifndef RS_UNSTABLE_EARLY
-#define RS_UNSTABLE_EARLY 1   // passes before the last rank by LDS atomics (not stable)
-#endif
 #define RS_MAXBINS 256
 #define RS_MAXTILES (2048 + 4096)   // tiles of a job: <= 2048 full ones + one partial per row
 #define RS_BLOCK 256
@@ -554,104 +525,6 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
     }
 }
 
-#if RS_SEGSORT
-// Two-digit sorts run MSD-first: the high digit by the (unstable) tiled pass
-// above, then every (row, high digit) segment on its own by the low digit
-// (k_rs_segsort): one block per segment counts its low digits in LDS and
-// places each entry by an LDS atomic — no global histogram, no stable
-// ranking (equal keys are interchangeable in the MSM).
-// Segment table: per row (first tile rowfirst[r]) and high digit d,
-// seg[2 (r bins + d)] = start, [+1] = length, from the pass's tile histograms.
-__global__ __launch_bounds__(256) void k_rs_segs(const uint32_t *__restrict__ hist, const uint32_t *__restrict__ total,
-                                                 const uint32_t *__restrict__ tiles,
-                                                 const uint32_t *__restrict__ rowfirst, uint32_t nt, uint32_t bins,
-                                                 uint32_t *__restrict__ seg) {
-    __shared__ uint32_t sc_[256];
-    const uint32_t row = blockIdx.x, t = threadIdx.x;
-    const uint32_t *TL = tiles + 5 * rowfirst[row];
-    const uint32_t r0 = TL[2], r1 = TL[3], rstart = TL[4];
-    uint32_t cnt = 0;
-    if (t < bins) cnt = (r1 < nt ? hist[t * nt + r1] : total[t]) - hist[t * nt + r0];
-    sc_[t] = cnt;
-    __syncthreads();
-    for (uint32_t d = 1; d < 256; d <<= 1) {
-        const uint32_t a = t >= d ? sc_[t - d] : 0u;
-        __syncthreads();
-        sc_[t] += a;
-        __syncthreads();
-    }
-    if (t < bins) {
-        seg[2 * ((size_t)row * bins + t)] = rstart + sc_[t] - cnt;
-        seg[2 * ((size_t)row * bins + t) + 1] = cnt;
-    }
-}
-// One block per segment. Segments of up to RS_SEG_LDS entries are held in
-// registers, ranked by LDS atomics, placed in LDS and written out in order
-// (coalesced); longer ones (structured scalars) are placed straight into
-// global memory.
-#define RS_SEG_LDS 8192
-template <int LBITS>
-__global__ __launch_bounds__(256) void k_rs_segsort(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
-                                                    const uint32_t *__restrict__ seg, uint32_t *__restrict__ kout,
-                                                    uint32_t *__restrict__ vout) {
-    constexpr uint32_t LB = 1u << LBITS;
-    constexpr int PER = RS_SEG_LDS / 256;
-    __shared__ uint32_t cnt[LB], off[LB];
-    __shared__ uint32_t lk[RS_SEG_LDS], lv[RS_SEG_LDS];
-    const uint32_t t = threadIdx.x;
-    const uint32_t s0 = seg[2 * (size_t)blockIdx.x], n = seg[2 * (size_t)blockIdx.x + 1];
-    if (n == 0) return;
-    if (t < LB) cnt[t] = 0;
-    __syncthreads();
-    const bool small = n <= RS_SEG_LDS;
-    uint32_t kr[PER], vr[PER];
-    if (small) {
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            const uint32_t i = j * 256 + t;
-            kr[j] = i < n ? kin[s0 + i] : 0u;
-            vr[j] = i < n ? vin[s0 + i] : 0u;
-            if (i < n) atomicAdd(&cnt[kr[j] & (LB - 1)], 1u);
-        }
-    } else {
-        for (uint32_t i = t; i < n; i += 256) atomicAdd(&cnt[kin[s0 + i] & (LB - 1)], 1u);
-    }
-    __syncthreads();
-    if (t < LB) off[t] = cnt[t];
-    __syncthreads();
-    for (uint32_t d = 1; d < LB; d <<= 1) {   // inclusive scan -> exclusive starts
-        const uint32_t a = (t < LB && t >= d) ? off[t - d] : 0u;
-        __syncthreads();
-        if (t < LB) off[t] += a;
-        __syncthreads();
-    }
-    if (t < LB) off[t] -= cnt[t];
-    __syncthreads();
-    if (small) {
-#pragma unroll
-        for (int j = 0; j < PER; j++) {
-            const uint32_t i = j * 256 + t;
-            if (i < n) {
-                const uint32_t pos = atomicAdd(&off[kr[j] & (LB - 1)], 1u);
-                lk[pos] = kr[j];
-                lv[pos] = vr[j];
-            }
-        }
-        __syncthreads();
-        for (uint32_t i = t; i < n; i += 256) {
-            kout[s0 + i] = lk[i];
-            vout[s0 + i] = lv[i];
-        }
-        return;
-    }
-    for (uint32_t i = t; i < n; i += 256) {
-        const uint32_t key = kin[s0 + i], val = vin[s0 + i];
-        const uint32_t pos = atomicAdd(&off[key & (LB - 1)], 1u);
-        kout[s0 + pos] = key;
-        vout[s0 + pos] = val;
-    }
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // Run reduction over the sorted entries, by fixed chunks of RBK_T entries per
@@ -722,37 +595,18 @@ template <bool NEGC> DEVI void msm_init_loaded(ge &acc, gec &p, bool neg) {
 }
 
 // FIRST: entries are (key, signed base index) and the gather of entry i+1 is
-// issued before entry i's addition (two base registers used in turn, so no
-// copy between them); otherwise entries are slots (key or key|RBK_FILL,
-// extended point at the same index) of the previous pass.
-// Latency-bound point kernels (run merges, the final run sums): compiled for
-// BPG_LAT_WAVES waves per SIMD. Capping them at 4 (128 VGPRs, so they hold
-// fewer registers while waiting on loads next to other streams' VALU-bound
-// kernels) measured no gain (70.6 vs 70.9 M, profiles/r02s_ab_latwaves.txt).
-#ifndef RBK_MERGE_PREFETCH
-#define RBK_MERGE_PREFETCH 0   // 1: merge passes load the next real slot's point ahead (no gain measured, profiles/r02u_ab_merge_prefetch.txt)
-#endif
-#ifndef BPG_LAT_WAVES
-#define BPG_LAT_WAVES 1
-#endif
-// RBK_PINGPONG: entry i+1's base is gathered into the other of two base
-// registers (no copy, more VGPRs); else into the one just consumed.
-#ifndef RBK_PINGPONG
-#define RBK_PINGPONG 0
-#endif
-// RBK_FRESH0: a run's first point is converted or copied instead of being
-// added to the identity (pass-1 entry 0, merge passes, final run sums, comb fold)
-#ifndef RBK_FRESH0
-#define RBK_FRESH0 1
-#endif
-#ifndef RBK_CWAVES
-#define RBK_CWAVES 2   // waves per SIMD of pass 1 over cached (folded) bases
-#endif
-#ifndef RBK_WAVES
-#define RBK_WAVES (RBK_PINGPONG ? 2 : 3)   // waves per SIMD the run reduction is compiled for
-#endif
+// issued before entry i's addition; otherwise entries are slots (key or
+// key|RBK_FILL, extended point at the same index) of the previous pass. A
+// run's first point is converted or copied instead of being added to the
+// identity (pass-1 entry 0 at 1M instead of 7M / 8M).
+// Waves per SIMD each pass is compiled for: pass 1 over affine Niels bases 3
+// (155 VGPRs; 4 spills 88 B per lane and measured slower,
+// profiles/r02zz_ab_pass1_w4.txt), over cached bases 2, the latency-bound
+// merge passes and final run sums 1 (capping them at 4 waves measured no
+// gain, profiles/r02s_ab_latwaves.txt).
+static constexpr int RBK_WAVES = 3, RBK_CWAVES = 2, RBK_LAT_WAVES = 1;
 template <bool FIRST, int FMT, bool NEGC>
-__global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACHED ? RBK_CWAVES : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
+__global__ __launch_bounds__(RBK_BLOCK, !FIRST ? RBK_LAT_WAVES : FMT == MSM_CACHED ? RBK_CWAVES : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         const ge *__restrict__ pin, SegTab T, uint64_t E,
                                                         uint32_t invalid, int cw, uint32_t *__restrict__ kout,
@@ -806,53 +660,33 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
     };
     if constexpr (FIRST) {
         typedef typename BaseOf<FMT>::T BT;
-        BT pa, pb;
+        BT pa;
         const uint32_t *skt = sk + rbk_lds(t * RBK_T), *svt = sv + rbk_lds(t * RBK_T);   // chunk has no pad inside
         if (!rbk_trash(first, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[0]);
-        // entry i: its base is in `use`; entry i+1's gather goes to `fill`.
-        // Returns false at the chunk's end (padding key).
-        auto step = [&](uint32_t i, BT &use, BT &fill) -> bool {
+        // entry 0 starts every lane's chunk from the identity (its own run or
+        // the open head), the same step for the whole wave: its base is
+        // converted, not added
+        {
+            BT use = pa;
+            const uint32_t kn = RBK_KEY(skt[1]);
+            if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[1]);
+            if (!rbk_trash(first, cw)) { msm_init_loaded<NEGC>(acc, use, svt[0] >> 31); real = true; }
+        }
+        // entry i: its base is in `use`; entry i+1's gather goes to pa
+        for (uint32_t i = 1; i < RBK_T; i++) {
+            BT use = pa;
             const uint32_t k = RBK_KEY(skt[i]);
-            if (k == invalid) return false;
+            if (k == invalid) break;
             if (k != cur) close_run(k);
             const uint32_t v = svt[i];
             if (i + 1 < RBK_T) {
                 const uint32_t kn = RBK_KEY(skt[i + 1]);
-                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(fill, sptr, svt[i + 1]);
+                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[i + 1]);
             }
             // zero digits (trash, sorted to the end of their row) are never added
             if (!rbk_trash(k, cw)) { msm_add_loaded<NEGC>(acc, use, v >> 31); real = true; }
-            return true;
-        };
-#if RBK_PINGPONG
-        static_assert(RBK_T % 2 == 0, "chunk of an even number of entries");
-        for (uint32_t i = 0; i < RBK_T; i += 2) {
-            if (!step(i, pa, pb)) break;
-            if (!step(i + 1, pb, pa)) break;
         }
-#else
-        uint32_t i0 = 0;
-#if RBK_FRESH0
-        // entry 0 starts every lane's chunk from the identity (its own run or
-        // the open head), the same step for the whole wave: its base is
-        // converted, not added (1M instead of 7M / 8M)
-        {
-            BT use = pa;
-            if (RBK_T > 1) {
-                const uint32_t kn = RBK_KEY(skt[1]);
-                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[1]);
-            }
-            if (!rbk_trash(first, cw)) { msm_init_loaded<NEGC>(acc, use, svt[0] >> 31); real = true; }
-            i0 = 1;
-        }
-#endif
-        for (uint32_t i = i0; i < RBK_T; i++) {
-            BT use = pa;
-            if (!step(i, use, pa)) break;
-        }
-        (void)pb;
-#endif
-    } else if (!RBK_MERGE_PREFETCH) {
+    } else {
         for (uint32_t i = 0; i < RBK_T; i++) {
             const uint32_t x = sk[rbk_lds(t * RBK_T + i)];
             const uint32_t k = RBK_KEY(x);
@@ -860,36 +694,8 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
             if (k != cur) close_run(k);
             if (!(x & RBK_FILL)) {
                 ge p; ge_load(p, pin + gs + i);
-                if (real || !RBK_FRESH0) ge_add(acc, acc, p);
+                if (real) ge_add(acc, acc, p);
                 else acc = p;              // the run's first piece: acc is the identity
-                real = true;
-            }
-        }
-    } else {
-        // slots of the previous pass: the point of the next real slot (not a
-        // filler) is in flight while the current one is added
-        const uint32_t *skt = sk + rbk_lds(t * RBK_T);
-        auto next_real = [&](uint32_t j) -> uint32_t {
-            for (; j < RBK_T; j++) {
-                const uint32_t x = skt[j];
-                if (RBK_KEY(x) == invalid) return RBK_T;
-                if (!(x & RBK_FILL)) return j;
-            }
-            return RBK_T;
-        };
-        uint32_t nr = next_real(0);
-        ge pn;
-        if (nr < RBK_T) ge_load(pn, pin + gs + nr);
-        for (uint32_t i = 0; i < RBK_T; i++) {
-            const uint32_t k = RBK_KEY(skt[i]);
-            if (k == invalid) break;
-            if (k != cur) close_run(k);
-            if (i == nr) {
-                const ge p = pn;
-                nr = next_real(i + 1);
-                if (nr < RBK_T) ge_load(pn, pin + gs + nr);
-                if (real || !RBK_FRESH0) ge_add(acc, acc, p);
-                else acc = p;
                 real = true;
             }
         }
@@ -909,7 +715,7 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? BPG_LAT_WAVES : FMT == MSM_CACH
 }
 // After the last pass: the head slot of each run sums the run's real pieces
 // and owns the bucket (serial; long only for giant runs of structured digits).
-__global__ __launch_bounds__(64, BPG_LAT_WAVES) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
+__global__ __launch_bounds__(64, RBK_LAT_WAVES) void k_rbk_final(const uint32_t *__restrict__ keys, const ge *__restrict__ pts,
                                                   uint64_t E, uint32_t invalid, int cw, ge *__restrict__ buckets,
                                                   uint8_t *__restrict__ bflag) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -923,7 +729,7 @@ __global__ __launch_bounds__(64, BPG_LAT_WAVES) void k_rbk_final(const uint32_t 
     for (uint64_t j = i; j < E && RBK_KEY(keys[j]) == k; j++) {
         if (keys[j] & RBK_FILL) continue;
         ge_load(p, pts + j);
-        if (real || !RBK_FRESH0) ge_add(acc, acc, p);
+        if (real) ge_add(acc, acc, p);
         else acc = p;
         real = true;
     }
@@ -940,12 +746,7 @@ DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict
 // kernels of other streams for up to a millisecond, so every register they do
 // not need is room for another wave of those (ROW_WAVES / BSEG_WAVES: waves
 // per SIMD compiled for).
-#ifndef BSEG_WAVES
-#define BSEG_WAVES 3
-#endif
-#ifndef ROW_WAVES
-#define ROW_WAVES 1
-#endif
+static constexpr int BSEG_WAVES = 3, ROW_WAVES = 1;
 __global__ __launch_bounds__(64, BSEG_WAVES) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
                                                    uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
                                                    ge *__restrict__ segA, ge *__restrict__ segT) {
@@ -1035,121 +836,6 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
     }
 }
 
-// Window rows in two launches spread over many blocks (ROW_TWO_LEVEL=1;
-// default k_bucket_seg + k_row_reduce above, one block per row). The
-// two-level form cuts a 2^15-bucket row's latency from ~270 to ~85 us of
-// serial point additions but adds ~35% more additions (the block scans),
-// and with the chip full of other streams' work the added VALU work costs
-// more than the latency it hides.
-// Row r is cut into SB blocks of B threads, thread t of block beta owning the
-// L buckets [s L, s L + L) of segment s = beta B + t:
-//   A_s = sum_j (j+1) S_{sL+j},  T_s = sum_j S_{sL+j}   (running sum, 2L adds)
-//   R = sum_s A_s + L sum_s s T_s
-//     = sum_beta Bb_beta + B L sum_beta beta U_beta, with
-//   Bb_beta = sum_t A_t + L sum_{t>=1} suf_t,  U_beta = suf_0,
-// suf_t = sum_{u>=t} T_u the block's inclusive suffix scan (sum_t t T_t =
-// sum_{t>=1} suf_t). k_row_blocks writes (Bb, U) per block; k_row_final does
-// the same weighted combine over the SB blocks of a row (one wave per row).
-#ifndef ROW_TWO_LEVEL
-#define ROW_TWO_LEVEL 0   // measured slower: 69.3 / 69.4 vs 71.8 / 71.8 M (profiles/r03b_ab_row_two_level.txt)
-#endif
-#define ROW_MAX_THREADS 4096   // threads per row (segments of L = half / 4096 buckets at c = 16)
-__global__ __launch_bounds__(256) void k_row_blocks(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
-                                                    uint32_t half, uint32_t L, int lgL, uint32_t SB, uint32_t nmsm,
-                                                    uint32_t W, ge *__restrict__ blkB, ge *__restrict__ blkU,
-                                                    ge *__restrict__ rows_out) {
-    __shared__ ge sh[256];
-    const uint32_t B = blockDim.x, t = threadIdx.x;
-    const uint32_t row = blockIdx.x / SB, beta = blockIdx.x % SB;
-    const size_t b0 = (size_t)row * half + ((size_t)beta * B + t) * L;
-    ge run, acc, p;
-    bucket_load(run, buckets, bflag, b0 + L - 1);
-    acc = run;
-    for (int j = (int)L - 2; j >= 0; j--) {
-        bucket_load(p, buckets, bflag, b0 + j);
-        ge_add(run, run, p);
-        ge_add(acc, acc, run);
-    }
-    // inclusive suffix scan of T (= run) over the block's threads
-    ge_store(&sh[t], run);
-    for (uint32_t d = 1; d < B; d <<= 1) {
-        __syncthreads();
-        ge a, b;
-        const bool act = t + d < B;
-        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
-        __syncthreads();
-        if (act) ge_store(&sh[t], a);
-    }
-    __syncthreads();
-    ge suf;
-    ge_load(suf, &sh[t]);
-    ge U;
-    if (t == 0) U = suf;
-    if (t > 0) {
-        ge_dbl_n(suf, lgL);   // L suf_t
-        ge_add(acc, acc, suf);
-    }
-    __syncthreads();
-    ge_store(&sh[t], acc);
-    for (uint32_t w = B / 2; w >= 1; w >>= 1) {
-        __syncthreads();
-        if (t < w) {
-            ge a, b;
-            ge_load(a, &sh[t]); ge_load(b, &sh[t + w]);
-            ge_add(a, a, b);
-            ge_store(&sh[t], a);
-        }
-    }
-    if (t == 0) {
-        ge r; ge_load(r, &sh[0]);
-        if (SB == 1) {
-            ge_store(rows_out + row_perm(row, nmsm, W), r);
-        } else {
-            ge_store(blkB + blockIdx.x, r);
-            ge_store(blkU + blockIdx.x, U);
-        }
-    }
-}
-__global__ __launch_bounds__(64) void k_row_final(const ge *__restrict__ blkB, const ge *__restrict__ blkU, uint32_t SB,
-                                                  int lgBL, uint32_t nmsm, uint32_t W, ge *__restrict__ rows_out) {
-    __shared__ ge sh[64];
-    const uint32_t row = blockIdx.x, t = threadIdx.x;
-    ge u, v;
-    if (t < SB) ge_load(u, blkU + (size_t)row * SB + t); else ge_identity(u);
-    ge_store(&sh[t], u);
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        __syncthreads();
-        ge a, b;
-        const bool act = t + d < 64;
-        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
-        __syncthreads();
-        if (act) ge_store(&sh[t], a);
-    }
-    __syncthreads();
-    if (t < SB) ge_load(v, blkB + (size_t)row * SB + t); else ge_identity(v);
-    if (t > 0 && t < SB) {
-        ge suf;
-        ge_load(suf, &sh[t]);
-        ge_dbl_n(suf, lgBL);   // B L suf_beta
-        ge_add(v, v, suf);
-    }
-    __syncthreads();
-    ge_store(&sh[t], v);
-    for (uint32_t w = 32; w >= 1; w >>= 1) {
-        __syncthreads();
-        if (t < w) {
-            ge a, b;
-            ge_load(a, &sh[t]); ge_load(b, &sh[t + w]);
-            ge_add(a, a, b);
-            ge_store(&sh[t], a);
-        }
-    }
-    if (t == 0) {
-        ge r; ge_load(r, &sh[0]);
-        ge_store(rows_out + row_perm(row, nmsm, W), r);
-    }
-}
-
 // Window width: lg(points) - 3 (measured best, profiles/r01 MSM window
 // sweeps), or another width in [4, 16] when a GF(p)-multiply count of the
 // job says it needs 3% fewer: W entries per point (7M Niels / 8M cached madd)
@@ -1167,16 +853,14 @@ static int msm_window(uint64_t total, int nmsm, int fmt) {
         const double W = (254 + w - 1) / w;
         return W * (double)total * madd + 2.0 * nmsm * W * (double)(1u << (w - 1)) * 9.0;
     };
-    // On by default since jobs hold four proofs' MSMs (nmsm = 8 for the IPP
-    // rounds, so the bucket term weighs 4x more): 82.7 / 83.1 vs 81.6 / 82.0 M
-    // constraints/s without it (profiles/r03o_ab_rowreduce_window_model.txt);
-    // at one proof per job it was neutral (74.0 / 74.6 vs 74.4 / 75.0 M,
-    // r03d_ab_window_model_threads.txt). BPG_MSM_WINDOW_MODEL=0: lg - 3 only.
-    static const bool model = [] { const char *e = getenv("BPG_MSM_WINDOW_MODEL"); return !(e && e[0] == '0'); }();
+    // Jobs hold four proofs' MSMs (nmsm = 8 for the IPP rounds, so the bucket
+    // term weighs 4x more): 82.7 / 83.1 vs 81.6 / 82.0 M constraints/s with
+    // lg - 3 only (profiles/r03o_ab_rowreduce_window_model.txt); at one proof
+    // per job it was neutral (r03d_ab_window_model_threads.txt).
     int best = c;
     for (int w = 4; w <= 16; w++)
         if (cost(w) < cost(best)) best = w;
-    return model && cost(best) < 0.97 * cost(c) ? best : c;
+    return cost(best) < 0.97 * cost(c) ? best : c;
 }
 
 MsmEngine::~MsmEngine() {
@@ -1197,11 +881,30 @@ void DBuf::grow(size_t need) {
     cap = n;
 }
 
+static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::grow's allocation
+size_t MsmEngine::bytes() const {
+    size_t b = 0;
+    for (const DBuf *d : {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_, &rk_a_, &rk_b_, &rp_a_, &rp_b_,
+                          &buckets_, &bflag_, &segacc_, &rows_dev_})
+        b += d->cap;
+    return b;
+}
+size_t MsmEngine::job_bytes(uint64_t total, int nmsm, int fmt) {
+    if (!total) return 0;
+    const int c = msm_window(total, nmsm, fmt), W = (254 + c - 1) / c;
+    const uint64_t rows = (uint64_t)nmsm * W, half = 1ull << (c - 1), E0 = (uint64_t)W * total;
+    const uint64_t capE = 2 * ((E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
+    const uint64_t nseg = half / std::min<uint64_t>(half, 8);
+    return 4 * grown(E0 * 4) + grown((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256) + grown((size_t)6 * RS_MAXTILES * 4) +
+           grown(capE * 4) + grown(capE * sizeof(ge)) + grown(capE + 1024) + grown((capE / 4 + 256) * sizeof(ge)) +
+           grown(rows * half * sizeof(ge)) + grown(rows * half) + grown(2 * rows * nseg * sizeof(ge)) +
+           grown(rows * sizeof(ge));
+}
 void MsmEngine::reserve(const MsmPlan &p) {
     size_t kb = p.E0 * 4;
     keys_.grow(kb); vals_.grow(kb); keys2_.grow(kb); vals2_.grow(kb);
-    // radix-sort tile histograms + totals, then the segment table (2 words per row and digit)
-    sort_tmp_.grow((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256 + (size_t)2 * RS_MAXBINS * p.rows * 4);
+    // radix-sort tile histograms + totals
+    sort_tmp_.grow((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256);
     rk_a_.grow(p.capE * 4); rp_a_.grow(p.capE * sizeof(ge));
     rk_b_.grow(p.capE * 4 / 4 + 1024); rp_b_.grow((p.capE / 4 + 256) * sizeof(ge));
     buckets_.grow((size_t)p.rows * p.half * sizeof(ge));
@@ -1214,42 +917,16 @@ void MsmEngine::reserve(const MsmPlan &p) {
 // a row; tiles_dev: nt x {start, end, first tile of the row, one past its last
 // tile, row start}); swaps the buffer pointers to the sorted pair.
 static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2, int key_bits, const uint32_t *tiles,
-                       uint32_t nt, const uint32_t *rowfirst, uint32_t rows, uint32_t *hist, uint32_t *seg,
-                       hipStream_t st) {
+                       uint32_t nt, uint32_t *hist, hipStream_t st) {
     if (!nt || key_bits < 1) return;
     // 8-bit digits only where they save a pass (their scatter costs more LDS)
     const int bits = (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
     const int passes = (key_bits + bits - 1) / bits;
-#if RS_SEGSORT
-    if (passes == 2 && key_bits >= 15) {   // the big jobs (c >= 15); small ones keep the tiled LSD passes
-        // high digit (bits [bits, key_bits), plus constant row bits) by the
-        // tiled pass, then each (row, high digit) segment by the low digit
-        const int shift = bits;
-        if (bits == 8) hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
-        else hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
-        hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nt, total);
-        if (bits == 8)
-            hipLaunchKernelGGL((k_rs_scatter<8, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
-                               total, k2, v2);
-        else
-            hipLaunchKernelGGL((k_rs_scatter<7, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
-                               total, k2, v2);
-        hipLaunchKernelGGL(k_rs_segs, dim3(rows), dim3(256), 0, st, hist, total, tiles, rowfirst, nt, bins, seg);
-        if (bits == 8)
-            hipLaunchKernelGGL(k_rs_segsort<8>, dim3(rows * bins), dim3(256), 0, st, k2, v2, seg, k, v);
-        else
-            hipLaunchKernelGGL(k_rs_segsort<7>, dim3(rows * bins), dim3(256), 0, st, k2, v2, seg, k, v);
-        BPG_HIP(hipGetLastError());
-        return;   // sorted pairs are back in (k, v)
-    }
-#else
-    (void)rowfirst; (void)rows; (void)seg;
-#endif
     for (int shift = 0; shift < key_bits; shift += bits) {
         // only the last of several passes must keep the order of equal digits
-        const bool last = passes > 1 && (!RS_UNSTABLE_EARLY || shift + bits >= key_bits);
+        const bool last = passes > 1 && shift + bits >= key_bits;
         if (bits == 8)
             hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         else
@@ -1326,13 +1003,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     p.capE = 2 * ((p.E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
     // buckets per first-level segment (k_bucket_seg): a row of `half`
     // buckets leaves half / seglen segments for the one-block row reduction,
-    // whose serial part is 3 additions per segment per thread
-    // (BPG_MSM_SEGLEN, a power of two; A/B)
-    static const uint32_t seg_cfg = [] {
-        const char *e = getenv("BPG_MSM_SEGLEN");
-        const uint32_t v = e ? (uint32_t)atoi(e) : 8u;
-        return v >= 2 && v <= 256 && (v & (v - 1)) == 0 ? v : 8u;
-    }();
+    // whose serial part is 3 additions per segment per thread (16 or 32
+    // measured 0.5-2% slower, profiles/r03j_ab_tskip_seglen.txt)
+    const uint32_t seg_cfg = 8;
     p.seglen = p.half < seg_cfg ? p.half : seg_cfg;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
@@ -1399,9 +1072,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
                        (uint32_t)nmsm, (uint32_t)p.half, keys, vals, geo);
     BPG_HIP(hipGetLastError());
-    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt,
-               (const uint32_t *)tiles_.p + 5 * nt, (uint32_t)p.rows, (uint32_t *)sort_tmp_.p,
-               (uint32_t *)sort_tmp_.p + (size_t)RS_MAXBINS * (RS_MAXTILES + 1) + 64, st_);
+    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
     uint64_t E = p.E0;
     const uint32_t *kin = keys;
@@ -1414,9 +1085,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
         ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"),
                      96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels;
-                     // each lane's first entry is a 1M conversion (RBK_FRESH0)
+                     // each lane's first entry is a 1M conversion
                      (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0 -
-                         (RBK_FRESH0 ? (fmt == MSM_CACHED ? 7.0 : 6.0) * (double)((p.E0 + RBK_T - 1) / RBK_T) : 0.0));
+                         (fmt == MSM_CACHED ? 7.0 : 6.0) * (double)((p.E0 + RBK_T - 1) / RBK_T));
         if (p.passes == 0 && fmt == MSM_NIELS && negc)
             hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, true>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
                                pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
@@ -1445,22 +1116,6 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     // the row kernel writes the window rows straight into the caller's pinned
     // buffer when it gives a device view of it (no copy launch per job)
     ge *rows_out = rows_direct ? reinterpret_cast<ge *>(rows_direct) : AS_GE(rows_dev_.p);
-#if ROW_TWO_LEVEL
-    {
-        // P threads per row (power of two), L buckets each, blocks of B <= 256
-        const uint32_t P = std::min<uint32_t>((uint32_t)p.half, ROW_MAX_THREADS);
-        const uint32_t L = (uint32_t)p.half / P, B = std::min<uint32_t>(P, 256), SB = P / B;
-        int lgL = 0, lgBL = 0;
-        while ((1u << lgL) < L) lgL++;
-        while ((1u << lgBL) < B * L) lgBL++;
-        ge *blkB = AS_GE(segacc_.p), *blkU = blkB + (size_t)p.rows * SB;
-        hipLaunchKernelGGL(k_row_blocks, dim3(p.rows * SB), dim3(B), 0, st_, AS_CGE(buckets_.p), bflag,
-                           (uint32_t)p.half, L, lgL, SB, (uint32_t)nmsm, (uint32_t)p.W, blkB, blkU, AS_GE(rows_out));
-        if (SB > 1)
-            hipLaunchKernelGGL(k_row_final, dim3(p.rows), dim3(64), 0, st_, (const ge *)blkB, (const ge *)blkU, SB,
-                               lgBL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out));
-    }
-#else
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
     ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
     hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
@@ -1469,7 +1124,6 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     while ((1 << lgL) < p.seglen) lgL++;
     hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
                        (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out));
-#endif
     BPG_HIP(hipGetLastError());
     if (!rows_direct)
         BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
@@ -1880,9 +1534,7 @@ DEVI void fold_pick(gec &t, const gec &t1, const gec &t3, const gec &t5, const g
     int m = d < 0 ? -d : d;
     if (m == 1) t = t1; else if (m == 3) t = t3; else if (m == 5) t = t5; else t = t7;
 }
-#ifndef BPG_FOLD_WAVES
-#define BPG_FOLD_WAVES 2
-#endif
+static constexpr int BPG_FOLD_WAVES = 2;
 // P: input point type (gen = affine Niels generators in round 0 of the
 // table-less path, gec = folded generators); the output is always cached.
 template <class P>
@@ -2004,9 +1656,7 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
 // point, which odd multiple, sign) is built on the host and read with scalar
 // loads; blocks never straddle a range.
 // ---------------------------------------------------------------------------
-#ifndef BPG_FOLD2_WNAF
-#define BPG_FOLD2_WNAF 3
-#endif
+static constexpr int BPG_FOLD2_WNAF = 3;   // odd multiples P, 3P of the three points in registers
 #define FOLD2_MAXSEG (2 * COMB_MAXRANGE)
 #define FOLD2_MAXOPS 400
 struct Fold2Args {
@@ -2206,15 +1856,14 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
 // per-block global table, word-major (lane-contiguous, so every table read
 // is coalesced); the next op's entry is loaded before the doublings.
 // ---------------------------------------------------------------------------
-#ifndef BPG_FOLD3_WNAF
-#define BPG_FOLD3_WNAF 4
-#endif
-static_assert(BPG_FOLD3_WNAF >= 3 && BPG_FOLD3_WNAF <= 5, "fold3 NAF width (odd multiples up to 15P)");
+// NAF width 4 (odd multiples P..7P); width 5 measured no better (fewer
+// additions, twice the table, profiles/r02w_ab_fold3_w5.txt)
+static constexpr int BPG_FOLD3_WNAF = 4;
 #define FOLDN_MAXSEG (2 * COMB_MAXRANGE)
 #define FOLDN_MAXOPS 640
-#define FOLDN_K 7
-#define FOLDN_MULT (1 << (BPG_FOLD3_WNAF - 2))        // odd multiples per point
-#define FOLDN_TABW (FOLDN_K * FOLDN_MULT * 40 * 64)   // table words per block
+static constexpr int FOLDN_K = 7;
+static constexpr int FOLDN_MULT = 1 << (BPG_FOLD3_WNAF - 2);           // odd multiples per point
+static constexpr uint32_t FOLDN_TABW = FOLDN_K * FOLDN_MULT * 40 * 64;  // table words per block
 struct FoldNArgs {
     const void *in[2];
     gec *out[2];
@@ -2235,12 +1884,9 @@ DEVI void foldn_get(gec &c, const uint32_t *tb) {
 #pragma unroll
     for (int k = 0; k < 40; k++) w[k] = tb[k * 64];
 }
-#ifndef FOLD3_WAVES
-#define FOLD3_WAVES 1      // waves per SIMD the triple fold is compiled for
-#endif
-#ifndef FOLD3_PREFETCH
-#define FOLD3_PREFETCH 1   // the next op's table entry is loaded before the doublings
-#endif
+// waves per SIMD the triple fold is compiled for (332 VGPRs; at 2 waves
+// it spilled and measured slower, profiles/r03c_ab_commitjob_fold3_smallmsm.txt)
+static constexpr int FOLD3_WAVES = 1;
 // the lane's odd multiples P, 3P, .. of the seven points into the block's
 // word-major table
 template <class P>
@@ -2285,7 +1931,7 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
-#if FOLD3_PREFETCH
+    // the next op's table entry is loaded before the doublings
     gec c;
     if (nops > 1) foldn_get(c, foldn_entry(tb, fold2_op(ops, 1)));
     for (uint32_t k = 1; k < nops; k++) {
@@ -2303,21 +1949,6 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
         c = cn;
     }
-#else
-    // no entry held across the doublings (40 fewer VGPRs): the entry's load
-    // latency is left to the other waves of the SIMD
-    for (uint32_t k = 1; k < nops; k++) {
-        const uint32_t op = fold2_op(ops, k);
-        const uint32_t g = op & 255;
-        if (g) {
-            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
-            ge_dbl_t<true>(acc, acc);
-        }
-        gec c;
-        foldn_get(c, foldn_entry(tb, op));
-        if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
-    }
-#endif
     const uint32_t tail = A.tail[sg];
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
@@ -2539,11 +2170,7 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
     {
         gen p;
         gen_load(p, reinterpret_cast<const gen *>(A.gens[v]) + i);
-#if RBK_FRESH0
         ge_from_niels(acc, p);   // identity + P_i (1M)
-#else
-        ge_identity(acc); ge_madd(acc, acc, p);
-#endif
     }
     for (int t = 0; t < 3; t++) {
         const uint32_t jj = i + (uint32_t)t * A.h1;

@@ -14,6 +14,9 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <map>
+#include <sched.h>
+#include <stdio.h>
 
 #include "r1cs_gpu.h"
 #include "statement.h"
@@ -127,16 +130,21 @@ void free_proof(struct ProofArtifacts *a) {
 }
 
 // ------------------------------------------------------------ inner ABI
+// Batched-prover pipeline layout (bpg_ctx_set_pipeline; 0 = automatic)
+struct Pipeline {
+    uint32_t producers = 0, lockstep = 0, max_inflight = 0;
+};
 struct bpg_ctx {
     int device;
     Strategy strat;   // IPP fold strategy of the calls made through this handle
+    Pipeline pipe;    // bpg_prove_batch layout of circuits prepared through it
 };
 bpg_ctx *bpg_ctx_create(int device) {
     return guarded([&]() -> bpg_ctx * {
         g_device = device;
         require_device();
         DeviceContext::get(device);
-        return new bpg_ctx{device, Strategy()};
+        return new bpg_ctx{device, Strategy(), Pipeline()};
     }, (bpg_ctx *)nullptr);
 }
 void bpg_ctx_destroy(bpg_ctx *ctx) { delete ctx; }
@@ -153,6 +161,11 @@ int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode) {
 int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes) {
     if (!ctx || lanes < -1) return -1;
     ctx->strat.ipp_tail = lanes;
+    return 0;
+}
+int bpg_ctx_set_pipeline(bpg_ctx *ctx, uint32_t producers, uint32_t lockstep, uint32_t max_inflight) {
+    if (!ctx || producers > 8 || lockstep > 4) return -1;
+    ctx->pipe = Pipeline{producers, lockstep, max_inflight};
     return 0;
 }
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
@@ -269,11 +282,15 @@ int bpg_point_sum(const uint8_t *points, uint32_t count, uint8_t out[32]) {
     }, -1);
 }
 
-struct bpg_prepared { std::unique_ptr<PreparedCS> p; };
+struct bpg_prepared {
+    std::unique_ptr<PreparedCS> p;
+    Pipeline pipe;
+};
 bpg_prepared *bpg_prepare(bpg_ctx *ctx, const bpg_r1cs_view *cs) {
     return guarded([&]() -> bpg_prepared * {
         bpg_prepared *b = new bpg_prepared();
         b->p = prepare_cs(cs, ctx->device, ctx->strat);
+        b->pipe = ctx->pipe;
         DeviceContext::get(ctx->device).gens(b->p->N);
         return b;
     }, (bpg_prepared *)nullptr);
@@ -375,11 +392,45 @@ struct Pool {
 Pool &pool() { static Pool *p = new Pool(); return *p; }
 }  // namespace
 
+// CPUs this process may use: the affinity mask, capped by a cgroup CPU
+// quota (cgroup v2 cpu.max). Producers are sized from it: each one keeps a
+// core busy drawing TranscriptRng streams.
+static uint32_t process_cpus() {
+    cpu_set_t set;
+    uint32_t n = 0;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (uint32_t)CPU_COUNT(&set);
+    if (!n) n = std::max(1u, std::thread::hardware_concurrency());
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long per = 0;
+        if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+            n = std::min<uint32_t>(n, std::max<uint32_t>(1, (uint32_t)(atol(q) / per)));
+        fclose(f);
+    }
+    return n;
+}
+static double since_ms(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+namespace {
+// Device bytes each pool thread's prover workspace held after its last batch
+// (per device): the consumers of the next batch reuse them, so HBM admission
+// counts them as available.
+std::mutex g_held_mu;
+std::map<int, std::vector<size_t>> g_held;
+// The last bpg_prove_batch's layout and pipeline counters (bpg_last_batch_stats)
+std::mutex g_bs_mu;
+double g_bs[BPG_BATCH_STATS] = {0};
+}  // namespace
+
 // Batched proving as a two-stage pipeline: producer threads
 // draw the TranscriptRng streams of 8 proofs at a time in lockstep (rng8)
-// into pinned slots, consumer threads drive the device part of each proof
-// on their own HIP stream. The RNG phase of later proofs overlaps the device
-// phase of earlier ones instead of alternating with it.
+// into device slots, consumer threads drive the device part of up to
+// `lockstep` proofs at once on their own HIP stream. The RNG phase of later
+// proofs overlaps the device phase of earlier ones instead of alternating
+// with it. Consumers are admitted by HBM: what free memory (plus the
+// workspaces the pool's consumers already hold) leaves after a reserve for a
+// verifier context, at consumer_bytes_estimate() each.
 int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, const uint8_t *entropy, uint32_t count,
                     uint32_t threads, uint8_t *proof_out, size_t proof_stride, size_t *lens) {
     return guarded([&]() -> int {
@@ -387,47 +438,58 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         const PreparedCS &cs = *p->p;
         if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
         if (threads == 0) threads = 1;
-        uint32_t groups = (count + 7) / 8;
-        // proofs per consumer step (BPG_LOCKSTEP, 1 to 4; default 4: the
-        // proofs' IPP MSM jobs merged, so the latency-bound launches after
-        // each job's first pass run once per four proofs. Measured at 24
-        // proofs in flight: 82.9 / 83.2 M constraints/s against 81.3 / 81.0
-        // for two per step and 75.9 / 70.5 for one,
-        // profiles/r03k_ab_lockstep4.txt, r03h_ab_lockstep_consumers.txt)
-        static const int lockstep = [] {
-            const char *e = getenv("BPG_LOCKSTEP");
-            const int v = e ? atoi(e) : 4;
-            return v < 1 ? 1 : v > 4 ? 4 : v;
-        }();
-        // producers: at most 8 (one lockstep group of 8 each); slots (device
-        // buffers) for the groups being drawn plus a queue per consumer. A
-        // producer draws ~20 proofs/s. One proof per consumer step: a third of
-        // the threads (24 -> 8 producers, 16 consumers); more: half of them
-        // (16 -> 8 producers, 8 consumers)
-        uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(groups, 8u),
-                                                              lockstep >= 2 ? threads / 2 : threads / 3));
-        if (const char *e = getenv("BPG_PRODUCERS")) {   // tuning override
-            int v = atoi(e);
-            if (v >= 1 && (uint32_t)v < threads) P = std::min<uint32_t>(groups, (uint32_t)v);
+        const auto t_start = std::chrono::steady_clock::now();
+        const uint32_t groups = (count + 7) / 8;
+        // proofs per consumer step (1 to 4; default 4: the proofs' IPP MSM
+        // jobs merged, so the latency-bound launches after each job's first
+        // pass run once per four proofs. Measured at 24 proofs in flight: 82.9
+        // / 83.2 M constraints/s against 81.3 / 81.0 for two per step and 75.9
+        // / 70.5 for one, profiles/r03k_ab_lockstep4.txt, r03h_ab_lockstep_consumers.txt)
+        const uint32_t L = p->pipe.lockstep ? p->pipe.lockstep : 4;
+        // producers: one lockstep group of 8 proofs each, at most 8, at most
+        // half of the threads and at most one per CPU of the process (a
+        // producer keeps a core busy; ~20 proofs/s each at 2^20)
+        uint32_t P = p->pipe.producers;
+        if (!P) P = std::max<uint32_t>(1, std::min<uint32_t>(threads / 2, process_cpus()));
+        P = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(P, 8), groups));
+        if (P >= threads && threads > 1) P = threads - 1;
+        const uint32_t C_req = std::max<uint32_t>(1, threads > P ? threads - P : 1);
+        uint32_t C = std::min<uint32_t>(C_req, (count + L - 1) / L);
+        // proofs in flight: at most max_inflight (default 24 at N = 2^20,
+        // scaled by 1/N: a proof in flight holds ~3.1 GB next to the 208 GB
+        // of comb tables, profiles/r03u_bench.json hbm_used_gb), and what
+        // HBM admits
+        const uint64_t cap2p20 = p->pipe.max_inflight ? p->pipe.max_inflight : 24;
+        const uint64_t inflight =
+            p->pipe.max_inflight ? cap2p20 : std::max<uint64_t>(1, (cap2p20 << 20) / std::max<uint32_t>(cs.N, 1));
+        C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(C, inflight / L));
+        BPG_HIP(hipSetDevice(cs.device));
+        size_t free_b = 0, total_b = 0;
+        BPG_HIP(hipMemGetInfo(&free_b, &total_b));
+        const size_t slot_bytes = 2 * (size_t)cs.n * 64 + 64;
+        const size_t est_c = consumer_bytes_estimate(cs, (int)L);
+        const size_t reserve = std::max<size_t>((size_t)2 << 30, total_b / 64) + verifier_bytes_estimate(cs);
+        uint32_t C_hbm = 0;
+        {
+            size_t held = 0, have_slots;
+            {
+                std::lock_guard<std::mutex> lk(g_held_mu);
+                const std::vector<size_t> &h = g_held[cs.device];
+                for (uint32_t id = P; id < P + C && id < h.size(); id++) held += h[id];
+            }
+            {
+                std::lock_guard<std::mutex> lk(cs.slot_mu);
+                have_slots = cs.slot_bytes >= slot_bytes ? cs.slot_bufs.size() : 0;
+            }
+            for (C_hbm = C; C_hbm > 1; C_hbm--) {
+                const size_t want_slots = std::min<size_t>(8 * (size_t)P + 2 * C_hbm, 8 * (size_t)groups);
+                const size_t new_slots = want_slots > have_slots ? (want_slots - have_slots) * slot_bytes : 0;
+                if ((double)C_hbm * est_c + new_slots + reserve <= (double)free_b + held) break;
+            }
         }
-        uint32_t C = std::max<uint32_t>(1, std::min<uint32_t>(count, threads > P ? threads - P : 1));
-        // proofs in flight, capped for HBM: a proof in flight holds ~3.1 GB
-        // at N = 2^20 (its buffers and its share of its stream's MSM
-        // scratch), next to 208 GB of comb tables: 24 of them keep the device
-        // at 292 GB of its 309 (BPG_MAX_INFLIGHT overrides; scales with 1/N)
-        static const uint32_t inflight_2p20 = [] {
-            const char *e = getenv("BPG_MAX_INFLIGHT");
-            const int v = e ? atoi(e) : 24;
-            return (uint32_t)(v < 1 ? 1 : v);
-        }();
-        const uint64_t inflight = std::max<uint64_t>(1, ((uint64_t)inflight_2p20 << 20) / std::max<uint32_t>(cs.N, 1));
-        C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(C, inflight / (uint64_t)lockstep));
-        uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
-        // BPG_HOST_SLOTS=1: producers write the draws into pinned host slots
-        // and each consumer copies its proof's draws up on its own stream, so
-        // the producers need no HIP streams (and hardware queues) at all
-        static const bool host_slots = [] { const char *e = getenv("BPG_HOST_SLOTS"); return e && e[0] == '1'; }();
-        std::vector<uint8_t *> slot = cs.slots(nslots, 2 * (size_t)cs.n * 64 + 64, host_slots);
+        C = std::min(C, C_hbm);
+        const uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
+        std::vector<uint8_t *> slot = cs.slots(nslots, slot_bytes);
         std::mutex mu;
         std::condition_variable cv;
         std::vector<int> free_slots;
@@ -436,8 +498,14 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         std::deque<uint32_t> ready;
         std::atomic<uint32_t> next_group(0);
         uint32_t producers_left = P;
-        bool abort = false;
+        bool abort = false, any_ready = false;
         std::string err;
+        // pipeline counters (ms, summed over threads): consumers waiting for
+        // a ready proof while producers were still drawing (after the first
+        // group: the pipeline fill is reported on its own), producers waiting
+        // for a free slot (the device is behind), producers drawing,
+        // consumers proving
+        double fill_ms = 0, starve_ms = 0, slot_wait_ms = 0, draw_ms = 0, prove_ms = 0;
         auto fail = [&](const std::string &e) {
             std::lock_guard<std::mutex> lk(mu);
             if (err.empty()) err = e;
@@ -446,6 +514,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         };
         std::vector<int> slot_of(count, -1);
         std::vector<ProveTimings> timings(count);
+        std::vector<size_t> held_after(P + C, 0);
         pool().run((int)(P + C), [&](int id) {
             try {
                 if ((uint32_t)id < P) {
@@ -455,7 +524,9 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                         uint32_t k0 = 8 * g, cnt = std::min<uint32_t>(8, count - k0);
                         {
                             std::unique_lock<std::mutex> lk(mu);
+                            const auto tw = std::chrono::steady_clock::now();
                             cv.wait(lk, [&] { return abort || free_slots.size() >= cnt; });
+                            slot_wait_ms += since_ms(tw);
                             if (abort) break;
                             for (uint32_t i = 0; i < cnt; i++) {
                                 slot_of[k0 + i] = free_slots.back();
@@ -467,11 +538,15 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                         for (uint32_t i = 0; i < cnt; i++) {
                             ent[i] = entropy + 32 * (size_t)(k0 + i);
                             blocks[k0 + i].wide = slot[slot_of[k0 + i]];
-                            blocks[k0 + i].on_device = !host_slots;
+                            blocks[k0 + i].on_device = true;
                             out[i] = &blocks[k0 + i];
                         }
-                        rng_draw_group(cs, label, label_len, ent, (int)cnt, out, !host_slots);
+                        const auto td = std::chrono::steady_clock::now();
+                        rng_draw_group(cs, label, label_len, ent, (int)cnt, out, true);
+                        const double dms = since_ms(td);
                         std::lock_guard<std::mutex> lk(mu);
+                        draw_ms += dms;
+                        if (!any_ready) { any_ready = true; fill_ms = since_ms(t_start); }
                         for (uint32_t i = 0; i < cnt; i++) ready.push_back(k0 + i);
                         cv.notify_all();
                     }
@@ -479,17 +554,19 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                     producers_left--;
                     cv.notify_all();
                 } else {
-                    // each consumer proves up to `lockstep` ready proofs at once
-                    // on its stream (gpu_prove_lockstep: one MSM job per step
-                    // for all of them)
+                    // each consumer proves up to L ready proofs at once on its
+                    // stream (gpu_prove_lockstep: one MSM job per step for all)
                     for (;;) {
                         uint32_t ks[4];
                         int nk = 0;
                         {
                             std::unique_lock<std::mutex> lk(mu);
+                            const auto tw = std::chrono::steady_clock::now();
+                            const bool filled = any_ready;
                             cv.wait(lk, [&] { return abort || !ready.empty() || producers_left == 0; });
+                            if (filled && (!ready.empty() || producers_left > 0)) starve_ms += since_ms(tw);
                             if (abort || ready.empty()) break;
-                            while (!ready.empty() && nk < lockstep) {
+                            while (!ready.empty() && nk < (int)L) {
                                 ks[nk++] = ready.front();
                                 ready.pop_front();
                             }
@@ -497,7 +574,9 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                         const RngBlock *rbs[4];
                         ProveTimings tms[4];
                         for (int i = 0; i < nk; i++) rbs[i] = &blocks[ks[i]];
+                        const auto tp = std::chrono::steady_clock::now();
                         std::vector<std::vector<uint8_t>> prs = gpu_prove_lockstep(cs, label, label_len, rbs, nk, tms);
+                        const double pms = since_ms(tp);
                         for (int i = 0; i < nk; i++) {
                             if (prs[i].size() > proof_stride) throw std::runtime_error("proof stride too small");
                             memcpy(proof_out + proof_stride * (size_t)ks[i], prs[i].data(), prs[i].size());
@@ -505,9 +584,11 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                             timings[ks[i]] = tms[i];
                         }
                         std::lock_guard<std::mutex> lk(mu);
+                        prove_ms += pms;
                         for (int i = 0; i < nk; i++) free_slots.push_back(slot_of[ks[i]]);
                         cv.notify_all();
                     }
+                    held_after[id] = thread_workspace_bytes(cs.device);
                 }
             } catch (const dev::HipError &e) {
                 fail(std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr);
@@ -515,10 +596,33 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                 fail(e.what());
             }
         });
+        {
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            std::vector<size_t> &h = g_held[cs.device];
+            if (h.size() < P + C) h.resize(P + C, 0);
+            for (uint32_t id = P; id < P + C; id++) h[id] = held_after[id];
+        }
+        const double wall = since_ms(t_start);
+        {
+            // host-bound: the consumers spent more than a tenth of their time
+            // after the pipeline fill waiting for producers
+            const double span = std::max(1e-9, (wall - fill_ms) * C);
+            std::lock_guard<std::mutex> lk(g_bs_mu);
+            const double v[BPG_BATCH_STATS] = {(double)P, (double)C, (double)L, (double)(C * L), wall, fill_ms,
+                                               starve_ms, slot_wait_ms, draw_ms, prove_ms,
+                                               starve_ms / span > 0.10 ? 1.0 : 0.0, free_b / 1e9, est_c / 1e9,
+                                               (double)C_req, (double)C_hbm, (double)process_cpus()};
+            memcpy(g_bs, v, sizeof(v));
+        }
         if (!err.empty()) throw std::runtime_error(err);
         last_timings() = timings[count - 1];   // the caller's thread reports the batch's last proof
         return 0;
     }, -1);
+}
+int bpg_last_batch_stats(double *out, int n) {
+    std::lock_guard<std::mutex> lk(g_bs_mu);
+    for (int i = 0; i < n && i < BPG_BATCH_STATS; i++) out[i] = g_bs[i];
+    return 0;
 }
 
 // prove.rs:37-82 for `count` distinct statements (include/bpg.h): CPU
@@ -538,6 +642,10 @@ static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector
     a->proof_cap = proof.size();
     return a;
 }
+namespace {
+std::mutex g_ss_mu;
+double g_ss[13] = {0};   // bpg_last_statements_stats
+}  // namespace
 int bpg_prove_statements(const char *name, const char *const *instances, const char *const *witnesses,
                          const char *const *gadgets, const uint64_t *seeds, uint32_t count, uint32_t threads,
                          struct ProofArtifacts **out) {
@@ -547,6 +655,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         if (!count) return 0;
         for (uint32_t k = 0; k < count; k++) out[k] = nullptr;
         const int device = g_device;
+        const auto t_start = std::chrono::steady_clock::now();
         const uint32_t W = std::max<uint32_t>(1, threads);
         const uint32_t C = std::min<uint32_t>(16, std::max<uint32_t>(1, W / 2));
         const size_t label_len = strlen(name);
@@ -558,11 +667,29 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             uint8_t entropy[32];
             RngBlock rb;
         };
+        BPG_HIP(hipSetDevice(device));
+        size_t free_b = 0, total_b = 0;
+        BPG_HIP(hipMemGetInfo(&free_b, &total_b));
+        size_t held = 0;
+        {
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            const std::vector<size_t> &h = g_held[device];
+            for (uint32_t id = W; id < W + C && id < h.size(); id++) held += h[id];
+        }
         std::mutex mu;
         std::condition_variable cv;
         std::deque<std::unique_ptr<Item>> prepared, ready;
-        uint32_t next = 0, synth_busy = 0, rng_busy = 0, inflight = 0, done = 0, proved = 0;
-        const uint32_t limit = W + 8 + 2 * C;
+        // prepared statements of finished proofs, recycled (device arrays and
+        // RNG slot kept: no hipMalloc / hipFree per statement)
+        std::vector<std::unique_ptr<PreparedCS>> spare;
+        uint32_t next = 0, synth_busy = 0, inflight = 0, done = 0, proved = 0;
+        // statements in flight (synthesised, prepared, drawn or being proved):
+        // at most W + 8 + 2C, and at most what HBM holds next to the
+        // consumers' workspaces, sized once the first statement is prepared
+        // (until then at most W)
+        uint32_t limit = W + 8 + 2 * C, hbm_limit = 0;
+        double est_st = 0;
+        double synth_ms = 0, prep_ms = 0, rng_ms = 0, prove_ms = 0, widle_ms = 0, cidle_ms = 0;
         std::string first_err;
         bool fatal = false;
         auto note_err = [&](uint32_t k, const std::string &e, bool hip) {
@@ -571,22 +698,26 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             if (hip) fatal = true;
             cv.notify_all();
         };
+        std::vector<size_t> held_after(W + C, 0);
         pool().run((int)(W + C), [&](int id) {
             const bool worker = (uint32_t)id < W;
             for (;;) {
                 std::vector<std::unique_ptr<Item>> group;
                 std::unique_ptr<Item> item;
+                std::unique_ptr<PreparedCS> reuse;
                 uint32_t k = 0;
                 int what = 0;   // 1 synthesise k, 2 RNG group, 3 device
                 {
                     std::unique_lock<std::mutex> lk(mu);
+                    const auto tw = std::chrono::steady_clock::now();
                     cv.wait(lk, [&] {
                         if (fatal || done == count) return true;
                         if (!worker) return !ready.empty();
                         const bool tail = next == count && synth_busy == 0;
                         if (prepared.size() >= 8 || (tail && !prepared.empty())) return true;
-                        return next < count && inflight < limit;
+                        return next < count && inflight < (est_st > 0 ? limit : W);
                     });
+                    (worker ? widle_ms : cidle_ms) += since_ms(tw);
                     if (fatal || done == count) break;
                     if (!worker) {
                         item = std::move(ready.front());
@@ -597,12 +728,12 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                             group.push_back(std::move(prepared.front()));
                             prepared.pop_front();
                         }
-                        rng_busy++;
                         what = 2;
                     } else {
                         k = next++;
                         synth_busy++;
                         inflight++;
+                        if (!spare.empty()) { reuse = std::move(spare.back()); spare.pop_back(); }
                         what = 1;
                     }
                 }
@@ -610,24 +741,29 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     std::unique_ptr<Item> it(new Item());
                     it->k = k;
                     bool ok = false;
+                    double ms_s = 0, ms_p = 0;
                     try {
                         EntropySource &e = thread_entropy();
                         const EntropySource saved = e;
                         if (seeds) { e.seeded = true; e.cs.seed(seeds[k]); }
                         try {
+                            const auto t0 = std::chrono::steady_clock::now();
                             Synthesis syn = synthesize_prover(instances[k], witnesses[k], gadgets[k]);
                             bpg_r1cs_view v = syn.cs->view(true);
-                            it->cs = prepare_cs(&v, device);
+                            ms_s = since_ms(t0);
+                            const auto t1 = std::chrono::steady_clock::now();
+                            it->cs = prepare_cs(&v, device, Strategy(), 0, 1, std::move(reuse));
                             for (size_t i = 0; i < syn.com_names.size(); i++)
                                 it->coms += syn.com_names[i] + " = 0x" + hex32(it->cs->V.data() + 32 * i) + "\n";
                             e.fill(it->entropy, 32);
+                            it->rb.wide = it->cs->slots(1, 2 * (size_t)it->cs->n * 64 + 64)[0];
+                            it->rb.on_device = true;
+                            ms_p = since_ms(t1);
                         } catch (...) {
                             e = saved;
                             throw;
                         }
                         e = saved;
-                        it->rb.wide = it->cs->slots(1, 2 * (size_t)it->cs->n * 64 + 64)[0];
-                        it->rb.on_device = true;
                         ok = true;
                     } catch (const dev::HipError &e) {
                         note_err(k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr, true);
@@ -636,10 +772,24 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     }
                     std::lock_guard<std::mutex> lk(mu);
                     synth_busy--;
+                    synth_ms += ms_s;
+                    prep_ms += ms_p;
+                    if (ok && est_st == 0) {
+                        // HBM budget of statements in flight: free memory and
+                        // the consumers' reusable workspaces, less C
+                        // one-proof workspaces and a reserve
+                        est_st = (double)prepared_bytes(*it->cs);
+                        const double reserve = std::max<double>(2.0 * (1 << 30), total_b / 64.0);
+                        const double avail = (double)free_b + (double)held - reserve -
+                                             (double)C * (double)consumer_bytes_estimate(*it->cs, 1);
+                        hbm_limit = (uint32_t)std::max<double>(std::min<double>(C + 8, limit), avail / est_st);
+                        limit = std::min(limit, hbm_limit);
+                    }
                     if (ok) prepared.push_back(std::move(it));
                     else { inflight--; done++; }
                     cv.notify_all();
                 } else if (what == 2) {
+                    const auto t0 = std::chrono::steady_clock::now();
                     try {
                         const PreparedCS *cs[8];
                         const uint8_t *ent[8];
@@ -656,11 +806,13 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     } catch (const std::exception &e) {
                         note_err(group[0]->k, e.what(), true);
                     }
+                    const double ms = since_ms(t0);
                     std::lock_guard<std::mutex> lk(mu);
-                    rng_busy--;
+                    rng_ms += ms;
                     for (auto &g : group) ready.push_back(std::move(g));
                     cv.notify_all();
                 } else {
+                    const auto t0 = std::chrono::steady_clock::now();
                     try {
                         std::vector<uint8_t> pr = gpu_prove_rng(*item->cs, label, label_len, item->rb);
                         out[item->k] = make_artifacts(item->coms, pr);
@@ -671,14 +823,35 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     } catch (const std::exception &e) {
                         note_err(item->k, e.what(), false);
                     }
-                    item.reset();   // frees the statement's device arrays
+                    const double ms = since_ms(t0);
                     std::lock_guard<std::mutex> lk(mu);
+                    prove_ms += ms;
+                    spare.push_back(std::move(item->cs));   // recycled by the next statement
+                    item.reset();
                     inflight--;
                     done++;
                     cv.notify_all();
                 }
             }
+            if (!worker) held_after[id] = thread_workspace_bytes(device);
         });
+        {
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            std::vector<size_t> &h = g_held[device];
+            if (h.size() < W + C) h.resize(W + C, 0);
+            for (uint32_t id = W; id < W + C; id++) h[id] = held_after[id];
+        }
+        spare.clear();   // the recycled statements' device memory, freed once per call
+        {
+            // the bounding stage: the device consumers waited for statements
+            // more than a tenth of their time -> the CPU workers
+            const double wall = since_ms(t_start);
+            const int bound = cidle_ms > 0.10 * wall * C ? 1 : 2;
+            const double v[13] = {(double)W, (double)C, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
+                                  widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9};
+            std::lock_guard<std::mutex> lk(g_ss_mu);
+            memcpy(g_ss, v, sizeof(v));
+        }
         if (fatal) {
             for (uint32_t k = 0; k < count; k++) { free_proof(out[k]); out[k] = nullptr; }
             throw std::runtime_error(first_err);
@@ -688,6 +861,11 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         if (n_ok < (int)count) g_err = first_err;   // guarded() cleared it on entry; keep the reason
         return n_ok;
     }, -1);
+}
+int bpg_last_statements_stats(double *out, int n) {
+    std::lock_guard<std::mutex> lk(g_ss_mu);
+    for (int i = 0; i < n && i < 13; i++) out[i] = g_ss[i];
+    return 0;
 }
 
 // Verifier::verify (verify.rs:71) over `count` proofs of one prepared

@@ -73,21 +73,10 @@ CombTables::~CombTables() {
     if (tabG) (void)hipFree(tabG);
     if (tabH) (void)hipFree(tabH);
 }
-static bool env_off(const char *name) {
-    const char *e = getenv(name);
-    return e && e[0] == '0';
-}
-bool Strategy::tables() const { return fold_tables >= 0 ? fold_tables != 0 : !env_off("BPG_FOLD_TABLES"); }
-bool Strategy::pairs() const { return fold_pairs >= 0 ? fold_pairs != 0 : !env_off("BPG_FOLD_PAIRS"); }
-uint32_t Strategy::tail() const {
-    if (ipp_tail >= 0) return (uint32_t)ipp_tail;
-    static const uint32_t env = [] { const char *e = getenv("BPG_IPP_TAIL"); return e ? (uint32_t)atoi(e) : 4096u; }();
-    return env;
-}
-int Strategy::group() const {
-    if (fold_pairs >= 0) return fold_pairs == 0 ? 1 : fold_pairs == 1 ? 2 : 3;
-    return env_off("BPG_FOLD_PAIRS") ? 1 : env_off("BPG_FOLD_TRIPLES") ? 2 : 3;
-}
+bool Strategy::tables() const { return fold_tables != 0; }
+bool Strategy::pairs() const { return fold_pairs != 0; }
+uint32_t Strategy::tail() const { return ipp_tail >= 0 ? (uint32_t)ipp_tail : 4096u; }
+int Strategy::group() const { return fold_pairs == 0 ? 1 : fold_pairs == 1 ? 2 : 3; }
 
 static std::mutex g_cache_mu;
 static std::string g_cache_dir;
@@ -412,9 +401,12 @@ struct Workspace : dev::ProfSink {
     }
 };
 
-Workspace &thread_workspace(int device) {
+static std::map<int, std::unique_ptr<Workspace>> &thread_workspaces() {
     static thread_local std::map<int, std::unique_ptr<Workspace>> wss;
-    auto &p = wss[device];
+    return wss;
+}
+Workspace &thread_workspace(int device) {
+    auto &p = thread_workspaces()[device];
     if (!p) {
         BPG_HIP(hipSetDevice(device));
         p.reset(new Workspace());
@@ -430,12 +422,43 @@ Workspace &thread_workspace(int device) {
     BPG_HIP(hipSetDevice(device));
     return *p;
 }
-
-// BPG_ZERO_COPY=0: copy the MSM rows and c_L / c_R down with hipMemcpyAsync
-// instead of writing them into pinned memory from the kernels (A/B switch)
-static bool zero_copy() {
-    static const bool on = [] { const char *e = getenv("BPG_ZERO_COPY"); return !(e && e[0] == '0'); }();
-    return on;
+size_t thread_workspace_bytes(int device) {
+    auto &m = thread_workspaces();
+    auto it = m.find(device);
+    if (it == m.end() || !it->second) return 0;
+    const Workspace &ws = *it->second;
+    size_t b = ws.msm ? ws.msm->bytes() : 0;
+    for (const DBuf *d : {&ws.w, &ws.yipm, &ws.zlo, &ws.zhi, &ws.ylo, &ws.yhi, &ws.tabs, &ws.mscal, &ws.partial,
+                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag})
+        b += d->cap;
+    for (const ProofBufs &B : ws.pb)
+        for (const DBuf *d : {&B.wide, &B.sL, &B.sR, &B.w, &B.wloc, &B.l1, &B.r0, &B.r1, &B.r3, &B.ypm, &B.yipm,
+                              &B.zlo, &B.zhi, &B.ylo, &B.yhi, &B.tabs, &B.a, &B.b, &B.mscal, &B.partial, &B.Gp[0],
+                              &B.Gp[1], &B.Hp[0], &B.Hp[1], &B.small, &B.wG, &B.wH, &B.wconv, &B.f3tab})
+            b += d->cap;
+    return b;
+}
+static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::grow's allocation
+// What gpu_prove_lockstep grows a workspace to for P proofs of `cs` (the
+// per-proof vectors, the IPP point buffers and the largest fold3 table, and
+// the MSM scratch of the largest job: rounds 0 and 1 cover 2 Nl points per
+// proof, the commitments 5 nl per proof in their own jobs).
+size_t consumer_bytes_estimate(const PreparedCS &cs, int P) {
+    const size_t S = sizeof(ScD), nl = cs.nl, Nl = cs.Nl;
+    const size_t per_proof = 6 * grown(nl * S + 64) + grown(cs.ncol * S + 64) + 4 * grown(Nl * S + 64) +
+                             grown((2 * Nl + 2) * S + 64) + 4 * grown(Nl / 2 * sizeof(PtD)) +
+                             grown(ipp_fold3_table_bytes((uint32_t)std::max<size_t>(Nl / 32, 64), COMB_MAXRANGE)) +
+                             ((size_t)8 << 20);
+    const size_t msm = std::max(MsmEngine::job_bytes(2 * (uint64_t)Nl * P, 2 * P, MSM_NIELS),
+                                MsmEngine::job_bytes(5 * (uint64_t)nl, 3, MSM_NIELS));
+    return (size_t)P * per_proof + msm;
+}
+// Verifier::verify of a circuit of cs's size on a fresh workspace: the
+// mega-MSM over 2N generators and the flattened / y^-i / g-h vectors.
+size_t verifier_bytes_estimate(const PreparedCS &cs) {
+    const size_t S = sizeof(ScD), N = cs.N;
+    return MsmEngine::job_bytes(2 * (uint64_t)N + 64, 1, MSM_NIELS) + grown(cs.ncol * S + 64) +
+           2 * grown(N * S) + grown(2 * N * S + 64) + grown((size_t)cs.n * S + 64) + ((size_t)64 << 20);
 }
 
 ProveTimings &last_timings() { static thread_local ProveTimings t; return t; }
@@ -471,8 +494,12 @@ PreparedCS::~PreparedCS() {
 }
 
 std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, const Strategy &strat, uint32_t rank,
-                                       uint32_t world) {
-    std::unique_ptr<PreparedCS> P(new PreparedCS());
+                                       uint32_t world, std::unique_ptr<PreparedCS> reuse) {
+    // a recycled PreparedCS keeps its device arrays and RNG slots (grow-only):
+    // no hipMalloc / hipFree per statement (a hipFree synchronises the device)
+    std::unique_ptr<PreparedCS> P = reuse && reuse->device == device ? std::move(reuse)
+                                                                      : std::unique_ptr<PreparedCS>(new PreparedCS());
+    P->huge_cols.clear();
     BPG_HIP(hipSetDevice(device));
     P->device = device;
     P->n = cs->n; P->m = cs->m; P->q = cs->q;
@@ -575,6 +602,15 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
     return P;
 }
 
+size_t prepared_bytes(const PreparedCS &cs) {
+    size_t b = 0;
+    for (const DBuf *d : {&cs.aL, &cs.aR, &cs.aO, &cs.vb_dev, &cs.col_ptr, &cs.col_row, &cs.col_coeff, &cs.short_cols,
+                          &cs.long_cols})
+        b += d->cap;
+    std::lock_guard<std::mutex> lk(cs.slot_mu);
+    return b + cs.slot_bufs.size() * cs.slot_bytes;
+}
+
 void gpu_pedersen(int device, const std::vector<Scalar> &v, const std::vector<Scalar> &vb, uint8_t *out) {
     DeviceContext &ctx = DeviceContext::get(device);
     Workspace &ws = thread_workspace(device);
@@ -673,38 +709,16 @@ static Transcript prover_transcript(const PreparedCS &cs, const uint8_t *label, 
 // forked from the transcript before any challenge, so all draws can be made
 // before the device work starts. Up to 8 proofs run in lockstep (Strobe8).
 // The producers' host-to-device copies (95 MB per 2^20 proof, a few GB/s in
-// all) go to one stream per producer thread (default), or with
-// BPG_PRODUCER_STREAMS=k to k streams shared by all producer threads. One
-// shared stream (fewer streams than hardware queues for the consumers)
-// measured 62.3 / 62.4 vs 70.8 / 69.7 M constraints/s with a stream per
-// producer (profiles/r03a_ab_producer_streams.txt).
-static hipStream_t shared_producer_stream(int device, int nstreams) {
-    static std::mutex mu;
-    static std::map<int, std::vector<hipStream_t>> streams;
-    static std::map<int, unsigned> next;
-    std::lock_guard<std::mutex> lk(mu);
-    std::vector<hipStream_t> &v = streams[device];
-    if ((int)v.size() < nstreams) {
-        hipStream_t s;
-        BPG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        v.push_back(s);
-        return s;
-    }
-    return v[next[device]++ % v.size()];
-}
+// all) go to one stream per producer thread: one stream shared by all
+// producers (fewer streams than hardware queues for the consumers) measured
+// 62.3 / 62.4 vs 70.8 / 69.7 M constraints/s (profiles/r03a_ab_producer_streams.txt).
 ProducerStage &producer_stage(int device) {
     static thread_local std::map<int, std::unique_ptr<ProducerStage>> m;
-    static const int nshared = [] { const char *e = getenv("BPG_PRODUCER_STREAMS"); return e ? atoi(e) : 0; }();
     auto &p = m[device];
     if (!p) {
         BPG_HIP(hipSetDevice(device));
         p.reset(new ProducerStage());
-        if (nshared > 0) {
-            p->st = shared_producer_stream(device, nshared);
-            p->owns_stream = false;
-        } else {
-            BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
-        }
+        BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
         for (int b = 0; b < 2; b++) {
             BPG_HIP(hipHostMalloc((void **)&p->host[b], (size_t)8 * ProducerStage::CHUNK * 64, hipHostMallocDefault));
             BPG_HIP(hipEventCreateWithFlags(&p->ev[b], hipEventBlockingSync | hipEventDisableTiming));
@@ -719,7 +733,7 @@ ProducerStage::~ProducerStage() {
         if (host[b]) (void)hipHostFree(host[b]);
         if (ev[b]) (void)hipEventDestroy(ev[b]);
     }
-    if (st && owns_stream) (void)hipStreamDestroy(st);
+    if (st) (void)hipStreamDestroy(st);
 }
 
 void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
@@ -931,19 +945,16 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     }
 
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G>, S1 = <s_L,G> + <s_R,H>
-    // (blinding terms added on the host): one MSM job, MSMs 3p .. 3p + 2
+    // (blinding terms added on the host): one MSM job of 3 MSMs per proof
     PtD *rowsA = ws.rows_host, *rowsLR = ws.rows_host + ROWS_HALF;
     // zero copy: the MSM row kernels and the c_L / c_R reductions write into
     // the pinned buffers through their device views (no copy launch per job)
-    const bool zc = zero_copy();
-    PtD *rowsA_dev = zc ? ws.rows_view : nullptr, *rowsLR_dev = zc ? ws.rows_view + ROWS_HALF : nullptr;
+    PtD *rowsA_dev = ws.rows_view, *rowsLR_dev = ws.rows_view + ROWS_HALF;
     const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
     const int64_t gneg = gs->N;             // their negations follow each vector
-    // one job for all P proofs' commitments, or one job per proof
-    // (BPG_LOCKSTEP_COMMIT=0, the default: a P-proof commitment job is the
-    // largest of the proof and sizes every workspace's MSM scratch — ~7 GB at
-    // P = 2 and 2^20 — so per-proof jobs leave HBM for more consumers)
-    static const bool one_commit_job = [] { const char *e = getenv("BPG_LOCKSTEP_COMMIT"); return e && e[0] == '1'; }();
+    // one commitment job per proof: a P-proof commitment job would be the
+    // largest of the proof and size every workspace's MSM scratch (~7 GB at
+    // P = 2 and 2^20), leaving HBM for fewer consumers
     const size_t ROWS_PER_PROOF = 192;   // 3 MSMs x at most 64 windows
     MsmPlan pA[MAX_LOCKSTEP] = {};
     {
@@ -965,26 +976,17 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             }
             launch_wide_reduce(wd, nl, world, rank, as<ScD>(B.sL), st);
             launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(B.sR), st);
-            const uint32_t m0 = 3 * (uint32_t)p;
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, m0, gneg};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, m0, gneg};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, m0 + 1, gneg};
-            seg[nseg++] = {as<ScD>(B.sL), G0, nl, m0 + 2, gneg};
-            seg[nseg++] = {as<ScD>(B.sR), H0, nl, m0 + 2, gneg};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg};
+            seg[nseg++] = {as<ScD>(B.sL), G0, nl, 2, gneg};
+            seg[nseg++] = {as<ScD>(B.sR), H0, nl, 2, gneg};
         }
-        if (nseg && (one_commit_job || P == 1)) {
-            int ph = ws.prof_begin("msm_commit", 5.0 * P * nl * (64 + 32));
-            pA[0] = ws.msm->enqueue(seg, nseg, 3 * P, rowsA, MSM_NIELS, rowsA_dev);
+        for (int p = 0; p < P && nseg; p++) {
+            int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
+            pA[p] = ws.msm->enqueue(seg + 5 * p, 5, 3, rowsA + ROWS_PER_PROOF * p, MSM_NIELS,
+                                    rowsA_dev + ROWS_PER_PROOF * p);
             ws.prof_end(ph);
-            for (int p = 1; p < P; p++) pA[p] = pA[0];
-        } else if (nseg) {
-            for (int p = 0; p < P; p++) {
-                for (int k = 0; k < 5; k++) seg[5 * p + k].msm -= 3 * (uint32_t)p;
-                int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
-                pA[p] = ws.msm->enqueue(seg + 5 * p, 5, 3, rowsA + ROWS_PER_PROOF * p, MSM_NIELS,
-                                        rowsA_dev ? rowsA_dev + ROWS_PER_PROOF * p : nullptr);
-                ws.prof_end(ph);
-            }
         }
     }
     ws.sync();
@@ -995,7 +997,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         Point AIS[3], tmp;
         if (nl) {
             const MsmPlan &pl = pA[p];
-            const PtD *rows = (one_commit_job || P == 1) ? rowsA + 3 * p * pl.W : rowsA + ROWS_PER_PROOF * p;
+            const PtD *rows = rowsA + ROWS_PER_PROOF * p;
             for (int k = 0; k < 3; k++) combine_rows(AIS[k], rows + k * pl.W, pl.W, pl.c);
         } else {
             pt_identity(AIS[0]); pt_identity(AIS[1]); pt_identity(AIS[2]);
@@ -1060,7 +1062,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         }
         for (DBuf *d : {&B.l1, &B.r0, &B.r1, &B.r3}) d->grow((size_t)nl * sizeof(ScD) + 64);
         B.small.grow(64 * sizeof(ScD));
-        ScD *dsmall = zc ? B.small_view + 1000 : as<ScD>(B.small);   // t_1..t_6, <w_V, v_blinding>
+        ScD *dsmall = B.small_view + 1000;   // t_1..t_6, <w_V, v_blinding> (pinned, device view)
         if (nl) {
             launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(B.sR), wL,
                             wR, wO, as<ScD>(B.ypm), as<ScD>(B.yipm), nl, as<ScD>(B.l1), as<ScD>(B.r0), as<ScD>(B.r1),
@@ -1072,7 +1074,6 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         }
         if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(B.partial), dsmall + 6, st);
         else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
-        if (!zc) BPG_HIP(hipMemcpyAsync(B.small_host + 1000, dsmall, 7 * sizeof(ScD), hipMemcpyDeviceToHost, st));
     }
     ws.sync();
     std::vector<Scalar> u(P), x(P), t_x(P), t_xb(P), e_bl(P), wch(P);
@@ -1202,7 +1203,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             A.lamG1 = mont(lam[p]); A.lamGu = mont(lam[p] * u[p]);
             A.muH1 = mont(mu[p]); A.muHu = mont(mu[p] * u[p]);
             ScD *ms = as<ScD>(B.mscal);
-            ScD *cout = zc ? B.small_view + 1020 : as<ScD>(B.small) + 60;   // c_L, c_R
+            ScD *cout = B.small_view + 1020;   // c_L, c_R (pinned, device view)
             const void *Gm = cur < 0 ? G0 : Gh[p], *Hm = cur < 0 ? H0 : Hh[p];
             const uint32_t L0 = 2 * (uint32_t)p, R0 = L0 + 1;   // this proof's L and R MSMs
             if (tail) {
@@ -1254,7 +1255,6 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                                       {ms + 2 * hh, Gm, nRG, R0, gn}, {ms + 3 * hh, at(Hm, h), h, R0, gn}};
                 for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
             }
-            if (!zc) BPG_HIP(hipMemcpyAsync(B.small_host + 1020, cout, 2 * sizeof(ScD), hipMemcpyDeviceToHost, st));
         }
         int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt, rowsLR_dev);

@@ -47,12 +47,12 @@ struct CombTables {
     size_t bytes = 0;
     ~CombTables();
 };
-// IPP fold strategy, per context (bpg_ctx_set_fold_tables / _pairs): -1
-// automatic (env BPG_FOLD_TABLES / BPG_FOLD_PAIRS = 0 disable, default on),
-// 0 off, 1 on. Proof bytes are identical under every strategy.
+// IPP fold strategy, per context (bpg_ctx_set_fold_tables / _pairs / _ipp_tail):
+// -1 default (tables on, round triples, tail at 4096 lanes), 0 off, 1 on.
+// Proof bytes are identical under every strategy.
 struct Strategy {
     int fold_tables = -1, fold_pairs = -1;
-    int ipp_tail = -1;   // IPP tail threshold in lanes (-1: env BPG_IPP_TAIL, else 4096)
+    int ipp_tail = -1;   // IPP tail threshold in lanes (-1: 4096)
     uint32_t tail() const;
     bool tables() const;
     bool pairs() const;
@@ -114,12 +114,24 @@ struct PreparedCS {
 
 // Build from a view. With cs->a_L == NULL the circuit is verifier-only.
 // world > 1: the prover's witness vectors are uploaded as this rank's slice.
+// reuse: a PreparedCS of an earlier statement whose device buffers and RNG
+// slots are recycled (grown if needed) instead of allocated anew.
 std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, const Strategy &strat = Strategy(),
-                                       uint32_t rank = 0, uint32_t world = 1);
+                                       uint32_t rank = 0, uint32_t world = 1,
+                                       std::unique_ptr<PreparedCS> reuse = nullptr);
+// Device bytes a prepared statement holds (its arrays and RNG slots).
+size_t prepared_bytes(const PreparedCS &cs);
 
 // Per-thread workspace (stream + buffers), grown on demand.
 struct Workspace;
 Workspace &thread_workspace(int device);
+// Device bytes held by the calling thread's workspace on `device` (0: none).
+size_t thread_workspace_bytes(int device);
+// HBM admission estimates: what a workspace proving P proofs of `cs` in
+// lockstep grows to, and what one Verifier::verify of a circuit of its size
+// needs on a fresh workspace.
+size_t consumer_bytes_estimate(const PreparedCS &cs, int P);
+size_t verifier_bytes_estimate(const PreparedCS &cs);
 
 struct ProveTimings { double rng_ms = 0, commit_ms = 0, vec_ms = 0, ipp_ms = 0, total_ms = 0; };
 
@@ -133,8 +145,7 @@ struct RngBlock {
 // Per-thread staging of RNG output into device buffers.
 struct ProducerStage {
     static const uint32_t CHUNK = 2048;   // draws per staged chunk
-    hipStream_t st = nullptr;                 // shared by producer threads unless owns_stream
-    bool owns_stream = true;
+    hipStream_t st = nullptr;                 // this producer thread's copy stream
     uint8_t *host[2] = {nullptr, nullptr};   // pinned, 8 x CHUNK x 64 B each
     hipEvent_t ev[2] = {nullptr, nullptr};
     ~ProducerStage();

@@ -41,6 +41,13 @@ struct CsBuffers {
     bool valid = false;
 };
 CsBuffers &cs_pool() { static thread_local CsBuffers b; return b; }
+// memset the optimiser may not drop (the buffer is reused, not freed, but the
+// intent is a wipe)
+void secure_wipe(void *p, size_t n) {
+    if (!p || !n) return;
+    memset(p, 0, n);
+    __asm__ __volatile__("" : : "r"(p) : "memory");
+}
 }  // namespace
 ConstraintSystem::ConstraintSystem(bool prover) : prover_(prover) {
     CsBuffers &b = cs_pool();
@@ -54,7 +61,20 @@ ConstraintSystem::ConstraintSystem(bool prover) : prover_(prover) {
     }
 }
 ConstraintSystem::~ConstraintSystem() {
+    // the witness (a_L, a_R, a_O and their byte forms) is wiped before its
+    // buffers go back to the thread's pool: the next recorder on this thread
+    // (a verifier's, say) must not inherit another statement's secrets
+    if (prover_) {
+        secure_wipe(aL_.data(), aL_.size() * sizeof(Scalar));
+        secure_wipe(aR_.data(), aR_.size() * sizeof(Scalar));
+        secure_wipe(aO_.data(), aO_.size() * sizeof(Scalar));
+        secure_wipe(aLb_.data(), aLb_.size());
+        secure_wipe(aRb_.data(), aRb_.size());
+        secure_wipe(aOb_.data(), aOb_.size());
+    }
     CsBuffers &b = cs_pool();
+    // retained capacity is bounded (a 2^22-gate statement's worth of terms)
+    if (term_coeff_.capacity() > ((size_t)32 << 22) * 3) return;
     if (b.valid && b.term_coeff.capacity() >= term_coeff_.capacity()) return;   // keep the larger set
     aL_.swap(b.aL); aR_.swap(b.aR); aO_.swap(b.aO);
     row_ptr_.swap(b.row_ptr); term_var_.swap(b.term_var); term_coeff_.swap(b.term_coeff);

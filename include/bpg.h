@@ -72,13 +72,27 @@ const char *bpg_last_error(void);
  * (release with free_proof), or NULL if statement k failed. `threads` CPU
  * workers synthesise and upload statements and draw the TranscriptRng
  * streams of up to 8 statements in lockstep; min(16, threads / 2) more
- * threads drive the device, one HIP stream each. Returns the number of
+ * threads drive the device, one HIP stream each. Statements in flight are
+ * capped by HBM (free memory next to the device threads' workspaces, at the
+ * footprint of the first prepared statement), and finished statements' device
+ * arrays are recycled for the next ones. Returns the number of
  * statements proved (bpg_last_error() names the first failure), < 0 on a
  * device error (then every out[k] is NULL). */
 int bpg_prove_statements(const char *name, const char *const *instances,
                          const char *const *witnesses, const char *const *gadgets,
                          const uint64_t *seeds, uint32_t count, uint32_t threads,
                          struct ProofArtifacts **out);
+
+/* Added: the last bpg_prove_statements of the process, per stage (ms summed
+ * over threads; out[i], i < n <= 13): [0] CPU workers, [1] device consumers,
+ * [2] statements in flight allowed, [3] wall ms, [4] synthesis ms, [5]
+ * prepare ms (transpose + upload + commitments), [6] TranscriptRng ms, [7]
+ * device prove ms, [8] worker idle ms, [9] consumer idle ms, [10] the
+ * bounding stage (1 CPU workers: consumers waited for statements more than a
+ * tenth of their time; 2 the device consumers), [11] statements in flight
+ * HBM admits (sized from the first prepared statement), [12] GB one prepared
+ * statement holds. */
+int bpg_last_statements_stats(double *out, int n);
 
 /* Added: `prover.num_constraints()` of the last c_prove on this thread
  * (the reference prints it from prove.rs:75; the CLI prints it here). */
@@ -298,19 +312,44 @@ int bpg_prove_prepared(bpg_prepared *p, const uint8_t *label, size_t label_len,
 /* Prove `count` independent proofs of one prepared circuit (proof k uses
  * entropy + 32*k and writes proof_out + k*proof_stride) with `threads`
  * host threads sharing the device. lens[k] receives each proof length.
- * Half of the threads (at most 8) draw the TranscriptRng streams, 8 proofs
- * at a time; each of the others proves four proofs at once on its own HIP
- * stream, their IPP MSM jobs merged (BPG_LOCKSTEP=1..4; 1: one proof per
- * stream, a third of the threads drawing). At most 24 * 2^20 / N proofs are
- * in flight (HBM: ~3.1 GB each at N = 2^20 next to the comb tables;
- * BPG_MAX_INFLIGHT), so extra threads stay idle. Proof bytes do not depend
- * on any of this.
+ * Producer threads draw the TranscriptRng streams, 8 proofs at a time (by
+ * default half of the threads, at most 8 and at most one per CPU the process
+ * may use: the affinity mask capped by a cgroup CPU quota); each of the
+ * other threads (consumers) proves up to four proofs at once on its own HIP
+ * stream, their IPP MSM jobs merged. Consumers are admitted by HBM: free
+ * device memory plus what the pool's consumer workspaces already hold, minus
+ * a reserve for a verifier context, at an estimated ~12 GB per consumer of
+ * four proofs at N = 2^20; and at most 24 * 2^20 / N proofs are in flight
+ * unless bpg_ctx_set_pipeline says otherwise. Extra threads stay idle. Proof
+ * bytes do not depend on any of this. bpg_last_batch_stats reports the
+ * layout used and whether the producers kept up.
  * Batch calls (this and bpg_verify_batch) run on one process-wide worker
  * pool: concurrent calls from several threads are safe and run one after
  * the other. */
 int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len,
                     const uint8_t *entropy, uint32_t count, uint32_t threads,
                     uint8_t *proof_out, size_t proof_stride, size_t *lens);
+
+/* Pipeline layout of bpg_prove_batch on circuits prepared through `ctx`
+ * afterwards (0 = automatic): `producers` TranscriptRng threads (1..8),
+ * `lockstep` proofs per consumer step (1..4, default 4), `max_inflight`
+ * proofs in flight (default 24 * 2^20 / N; HBM admission still applies).
+ * Returns 0, -1 on an out-of-range value. */
+int bpg_ctx_set_pipeline(bpg_ctx *ctx, uint32_t producers, uint32_t lockstep,
+                         uint32_t max_inflight);
+
+/* The last bpg_prove_batch of the process (out[i], i < n <= BPG_BATCH_STATS):
+ * [0] producers, [1] consumers, [2] proofs per consumer step, [3] proofs in
+ * flight, [4] wall ms, [5] ms until the first group of draws was ready (the
+ * pipeline fill), [6] consumer ms spent waiting for a ready proof while
+ * producers were still drawing (after the fill), [7] producer ms spent
+ * waiting for a free slot (the device was behind), [8] producer ms drawing,
+ * [9] consumer ms proving, [10] 1 if host-bound (consumers waited more than
+ * a tenth of their time after the fill), [11] free HBM at the start (GB),
+ * [12] estimated GB per consumer, [13] consumers the threads allowed,
+ * [14] consumers HBM admitted, [15] CPUs the process may use. */
+#define BPG_BATCH_STATS 16
+int bpg_last_batch_stats(double *out, int n);
 
 /* Verifier::verify (src/verify.rs:71) over `count` proofs of one circuit
  * prepared by bpg_prepare_verifier with `threads` host threads, each on its own HIP stream (config 5's

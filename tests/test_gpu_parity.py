@@ -203,6 +203,30 @@ def test_prepared_batch_matches_single(bpg, ctx, resources):
     assert len(set(proofs)) == 6
 
 
+@pytest.mark.parametrize("producers,lockstep", [(1, 1), (2, 2), (1, 3), (3, 4)])
+def test_batch_layouts_bit_exact(bpg, resources, producers, lockstep):
+    """The batched prover's pipeline layout (bpg_ctx_set_pipeline: RNG
+    producers, proofs per consumer step) never changes proof bytes: 11 proofs
+    (a partial RNG group of 8 and partial lockstep steps) equal single proofs,
+    and bpg_last_batch_stats reports the layout that ran."""
+    fx = read_fixture(os.path.join(resources, "or5"))
+    bpg.set_seed(2)
+    syn = bpg.Synth(fx["inst"], fx["wtns"], fx["gadgets"])
+    c = bpg.Context(0)
+    c.set_pipeline(producers=producers, lockstep=lockstep)
+    prep = c.prepare(syn.view)
+    ents = [bytes([k + 40]) * 32 for k in range(11)]
+    proofs = prep.prove_batch(b"layout", ents, threads=producers + 3)
+    st = bpg.last_batch_stats()
+    assert st["producers"] == producers and st["lockstep"] == lockstep and st["consumers"] >= 1
+    assert st["wall_ms"] > 0 and st["producer_draw_ms"] > 0 and st["consumer_prove_ms"] > 0
+    for k in (0, 5, 10):
+        assert proofs[k] == c.r1cs_prove(b"layout", syn.view, ents[k])[0]
+    assert len(set(proofs)) == 11
+    with pytest.raises(bpg.BpgError):
+        c.set_pipeline(producers=9)
+
+
 def test_verify_batch(bpg, ctx, resources):
     """bpg_verify_batch (config 5's batch verification): every valid proof of
     a batch accepted, each tampered one rejected, same verdicts as the single

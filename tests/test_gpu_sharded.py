@@ -6,8 +6,9 @@ across GPUs: one process per rank, partial sums exchanged by all-gather).
   layout) must be byte-identical, on every rank, to the single-process
   proof (bpg_r1cs_prove) and to the CPU oracle's;
 * at BASELINE's full sizes (config 4 = 2^18 at 2, 4 and 8 ranks; config 5
-  and the reference's merkle512 circuit, merkle_tree_gadget.rs:528, = 2^20 at
-  2 ranks) every rank's proof must equal the committed oracle proof of
+  = 2^20 at 2, 4 and 8 ranks, the 8-GPU split the north_star names; the
+  reference's merkle512 circuit, merkle_tree_gadget.rs:528, = 2^20 at 2 and
+  8 ranks) every rank's proof must equal the committed oracle proof of
   tests/golden/fullsize.json, with the comb tables and the round-triple folds
   of the one-GPU default running on every rank's slice (prove.rs:78-79);
 * the sharded verifier across processes, per call (bpg_r1cs_verify_shard)
@@ -120,10 +121,11 @@ def test_sharded_prove_small_ipp_tail(bpg, tmp_path, name, world, tail):
 
 
 @pytest.mark.parametrize("name,world", [("config4", 2), ("config4", 4), ("config4", 8), ("config5", 2),
-                                        ("merkle512", 2)])
+                                        ("config5", 4), ("config5", 8), ("merkle512", 2), ("merkle512", 8)])
 def test_sharded_prove_fullsize_golden(bpg, trimmed, tmp_path, name, world):
     """BASELINE config 4 (Pippenger MSM sharded over 1/2/4/8 GPUs) and the
-    2^20 statements: every rank's proof equals the committed oracle proof."""
+    2^20 statements split over up to 8 ranks: every rank's proof equals the
+    committed oracle proof."""
     res = run_ranks("golden:" + name, world, tmp_path, timeout=300)
     check_ranks(res)
     for r in res:

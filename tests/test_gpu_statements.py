@@ -43,3 +43,12 @@ def test_prove_statements_matches_c_prove(bpg):
         assert out[k][1] == want[1], "coms of statement %d" % k
         assert out[k][0] == want[0], "proof of statement %d" % k
         assert bpg.verify("stmts", st[0], out[k][0], out[k][1], st[2])
+    # per-stage counters of the call (bpg_last_statements_stats), and the HBM
+    # budget sized from the first prepared statement (statement buffers are
+    # recycled across the call's statements of different sizes above)
+    st = bpg.last_statements_stats()
+    assert st["workers"] == 6 and st["consumers"] == 3
+    assert st["est_gb_per_statement"] > 0 and st["hbm_limit"] >= st["consumers"] + 1
+    assert st["limit"] <= 6 + 8 + 2 * 3
+    assert st["bound_stage"] in ("cpu workers (synthesis + prepare + rng)", "device consumers")
+    assert st["synth_ms"] > 0 and st["prove_ms"] > 0 and st["rng_ms"] > 0
