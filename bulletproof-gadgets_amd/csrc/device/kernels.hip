@@ -663,6 +663,21 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? RBK_LAT_WAVES : FMT == MSM_CACH
         BT pa;
         const uint32_t *skt = sk + rbk_lds(t * RBK_T), *svt = sv + rbk_lds(t * RBK_T);   // chunk has no pad inside
         if (!rbk_trash(first, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[0]);
+        // entry i: its base is in `use`; entry i+1's gather goes to `fill`.
+        // Returns false at the chunk's end (padding key).
+        auto step = [&](uint32_t i, BT &use, BT &fill) -> bool {
+            const uint32_t k = RBK_KEY(skt[i]);
+            if (k == invalid) return false;
+            if (k != cur) close_run(k);
+            const uint32_t v = svt[i];
+            if (i + 1 < RBK_T) {
+                const uint32_t kn = RBK_KEY(skt[i + 1]);
+                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(fill, sptr, svt[i + 1]);
+            }
+            // zero digits (trash, sorted to the end of their row) are never added
+            if (!rbk_trash(k, cw)) { msm_add_loaded<NEGC>(acc, use, v >> 31); real = true; }
+            return true;
+        };
         // entry 0 starts every lane's chunk from the identity (its own run or
         // the open head), the same step for the whole wave: its base is
         // converted, not added
@@ -672,19 +687,9 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? RBK_LAT_WAVES : FMT == MSM_CACH
             if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[1]);
             if (!rbk_trash(first, cw)) { msm_init_loaded<NEGC>(acc, use, svt[0] >> 31); real = true; }
         }
-        // entry i: its base is in `use`; entry i+1's gather goes to pa
         for (uint32_t i = 1; i < RBK_T; i++) {
             BT use = pa;
-            const uint32_t k = RBK_KEY(skt[i]);
-            if (k == invalid) break;
-            if (k != cur) close_run(k);
-            const uint32_t v = svt[i];
-            if (i + 1 < RBK_T) {
-                const uint32_t kn = RBK_KEY(skt[i + 1]);
-                if (kn != invalid && !rbk_trash(kn, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[i + 1]);
-            }
-            // zero digits (trash, sorted to the end of their row) are never added
-            if (!rbk_trash(k, cw)) { msm_add_loaded<NEGC>(acc, use, v >> 31); real = true; }
+            if (!step(i, use, pa)) break;
         }
     } else {
         for (uint32_t i = 0; i < RBK_T; i++) {

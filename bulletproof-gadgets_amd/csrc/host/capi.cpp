@@ -129,6 +129,12 @@ void free_proof(struct ProofArtifacts *a) {
     free(a);
 }
 
+// Device bytes each pool thread's prover workspace held after its last batch
+// (per device): the consumers of the next batch reuse them, so HBM admission
+// counts them as available.
+static std::mutex g_held_mu;
+static std::map<int, std::vector<size_t>> g_held;
+
 // ------------------------------------------------------------ inner ABI
 // Batched-prover pipeline layout (bpg_ctx_set_pipeline; 0 = automatic)
 struct Pipeline {
@@ -178,24 +184,6 @@ int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
     for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
     return 0;
 }
-int64_t bpg_ctx_trim(bpg_ctx *ctx) {
-    return guarded([&]() -> int64_t {
-        if (!ctx) throw std::runtime_error("NULL context");
-        DeviceContext &c = DeviceContext::get(ctx->device);
-        std::lock_guard<std::mutex> lk(c.mu);
-        int64_t freed = 0;
-        for (auto e = c.combs.begin(); e != c.combs.end();) {
-            if (e->second.use_count() == 1) { freed += (int64_t)e->second->bytes; e = c.combs.erase(e); }
-            else ++e;
-        }
-        for (auto e = c.slices.begin(); e != c.slices.end();) {
-            if (e->second.use_count() == 1) e = c.slices.erase(e);
-            else ++e;
-        }
-        return freed;
-    }, (int64_t)-1);
-}
-
 int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity) {
     return guarded([&]() -> int {
         DeviceContext::get(ctx->device).gens(capacity);
@@ -372,6 +360,10 @@ struct Pool {
             });
         }
     }
+    int size() {
+        std::lock_guard<std::mutex> serial(run_mu);
+        return (int)workers.size();
+    }
     void run(int n, std::function<void(int)> f) {
         std::lock_guard<std::mutex> serial(run_mu);
         ensure(n);
@@ -389,8 +381,39 @@ struct Pool {
         for (auto &t : workers) t.detach();
     }
 };
-Pool &pool() { static Pool *p = new Pool(); return *p; }
 }  // namespace
+static Pool &pool() { static Pool *p = new Pool(); return *p; }
+
+int64_t bpg_ctx_trim(bpg_ctx *ctx) {
+    return guarded([&]() -> int64_t {
+        if (!ctx) throw std::runtime_error("NULL context");
+        DeviceContext &c = DeviceContext::get(ctx->device);
+        int64_t freed = 0;
+        {
+            std::lock_guard<std::mutex> lk(c.mu);
+            for (auto e = c.combs.begin(); e != c.combs.end();) {
+                if (e->second.use_count() == 1) { freed += (int64_t)e->second->bytes; e = c.combs.erase(e); }
+                else ++e;
+            }
+            for (auto e = c.slices.begin(); e != c.slices.end();) {
+                if (e->second.use_count() == 1) e = c.slices.erase(e);
+                else ++e;
+            }
+        }
+        // the worker pool's per-thread workspaces (streams, MSM scratch, proof
+        // buffers: ~12 GB per consumer of four 2^20 proofs) and the caller's
+        const int dev = ctx->device;
+        std::atomic<int64_t> ws(0);
+        const int nw = pool().size();
+        if (nw) pool().run(nw, [&](int) { ws += (int64_t)release_thread_workspace(dev); });
+        ws += (int64_t)release_thread_workspace(dev);
+        {
+            std::lock_guard<std::mutex> lk(g_held_mu);
+            g_held.erase(dev);
+        }
+        return freed + ws.load();
+    }, (int64_t)-1);
+}
 
 // CPUs this process may use: the affinity mask, capped by a cgroup CPU
 // quota (cgroup v2 cpu.max). Producers are sized from it: each one keeps a
@@ -413,11 +436,6 @@ static double since_ms(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 namespace {
-// Device bytes each pool thread's prover workspace held after its last batch
-// (per device): the consumers of the next batch reuse them, so HBM admission
-// counts them as available.
-std::mutex g_held_mu;
-std::map<int, std::vector<size_t>> g_held;
 // The last bpg_prove_batch's layout and pipeline counters (bpg_last_batch_stats)
 std::mutex g_bs_mu;
 double g_bs[BPG_BATCH_STATS] = {0};
@@ -914,10 +932,48 @@ int bpg_verify_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, co
 // and its draw rate (draws per second per thread for `lanes` proofs).
 int bpg_rng_selftest(void) {
     return guarded([&]() -> int {
+        // the permutations against the portable scalar Keccak-f[1600]
+        uint64_t x = 0x9e3779b97f4a7c15ULL;
+        for (int t = 0; t < 64; t++) {
+            uint64_t a[25], b[25];
+            for (int i = 0; i < 25; i++) {
+                x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+                a[i] = b[i] = x;
+            }
+            keccakf_scalar(a);
+            keccakf(b);   // the AVX-512 single-state form where available
+            if (memcmp(a, b, sizeof(a))) return 20;
+        }
+        {
+            // keccak8 lane k equals the scalar permutation of lane k's state
+            alignas(64) uint64_t L[25][8];
+            uint64_t ref[8][25];
+            for (int i = 0; i < 25; i++)
+                for (int k = 0; k < 8; k++) L[i][k] = ref[k][i] = 0x0123456789abcdefULL * (uint64_t)(i + 1) + (uint64_t)k * 0x1111;
+            keccak8(L);
+            for (int k = 0; k < 8; k++) {
+                keccakf_scalar(ref[k]);
+                for (int i = 0; i < 25; i++) if (L[i][k] != ref[k][i]) return 21;
+            }
+        }
         Transcript T((const uint8_t *)"selftest", 8);
         T.append_u64("m", 3);
         TranscriptRng base(T);
         base.rekey_with_witness_bytes("v_blinding", (const uint8_t *)"0123456789abcdef0123456789abcdef", 32);
+        {
+            // TranscriptRng::draw64 (constant-framing fast path) = fill_bytes
+            TranscriptRng r1(base), r2(base);
+            const uint8_t ent[32] = {7, 1, 2};
+            r1.finalize(ent);
+            r2.finalize(ent);
+            uint8_t a[64], b[64];
+            for (int d = 0; d < 300; d++) {
+                r1.fill_bytes(a, d % 7 == 3 ? 32 : 64);
+                if (d % 7 == 3) { r2.fill_bytes(b, 32); }
+                else r2.draw64(b);
+                if (memcmp(a, b, d % 7 == 3 ? 32 : 64)) return 22;
+            }
+        }
         for (int lanes = 1; lanes <= 8; lanes++) {
             uint8_t ent[8][32];
             const uint8_t *ep[8];

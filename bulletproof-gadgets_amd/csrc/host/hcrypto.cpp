@@ -448,7 +448,7 @@ static const uint64_t RC[24] = {
     0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
 #define ROL(x, s) (((x) << (s)) | ((x) >> (64 - (s))))
 // Keccak-f[1600], fully unrolled theta/rho/pi/chi/iota on 25 named lanes.
-void keccakf(uint64_t s[25]) {
+void keccakf_scalar(uint64_t s[25]) {
     uint64_t a00 = s[0], a01 = s[1], a02 = s[2], a03 = s[3], a04 = s[4];
     uint64_t a05 = s[5], a06 = s[6], a07 = s[7], a08 = s[8], a09 = s[9];
     uint64_t a10 = s[10], a11 = s[11], a12 = s[12], a13 = s[13], a14 = s[14];
@@ -479,6 +479,12 @@ void keccakf(uint64_t s[25]) {
     s[20] = a20; s[21] = a21; s[22] = a22; s[23] = a23; s[24] = a24;
 }
 #undef ROL
+// AVX-512 single-state permutation where the CPU has it (rng8.cpp:
+// keccakf_x1_avx512, ~1.6-2x the scalar speed); the scalar form otherwise
+void keccakf(uint64_t s[25]) {
+    if (have_avx512()) keccakf_x1_avx512(s);
+    else keccakf_scalar(s);
+}
 static inline void perm_bytes(uint8_t st[200]) {
     uint64_t w[25];
     memcpy(w, st, 200);   // little-endian host
@@ -577,6 +583,24 @@ void TranscriptRng::fill_bytes(uint8_t *d, size_t n) {
     uint8_t len[4]; u32le(len, (uint32_t)n);
     s.meta_ad(len, 4, false);
     s.prf(d, n, false);
+}
+// fill_bytes(d, 64) after another 64-byte draw (STROBE at pos 64, pos_begin
+// 0): meta_ad(len) + begin_op(I|A|C) + run_f only xor constant framing
+// bytes into words 8, 9 and 20 (DRAW64_W*), then the permutation, and the
+// 64 output bytes are read and zeroed. Identical to fill_bytes
+// (bpg_rng_selftest); any other state takes the general path.
+void TranscriptRng::draw64(uint8_t d[64]) {
+    if (s.pos != 64 || s.pos_begin != 0) { fill_bytes(d, 64); return; }
+    uint64_t *w = reinterpret_cast<uint64_t *>(s.st);
+    w[8] ^= DRAW64_W8;
+    w[9] ^= DRAW64_W9;
+    w[20] ^= DRAW64_W20;
+    keccakf(w);
+    memcpy(d, w, 64);
+    memset(w, 0, 64);
+    s.pos = 64;
+    s.pos_begin = 0;
+    s.cur_flags = F_I | F_A | F_C;
 }
 
 // ============================================================== chacha20

@@ -72,7 +72,16 @@ void pedersen_commit(uint8_t out[32], const Scalar &v, const Scalar &vb);
 void mul_var(Point &r, const Scalar &s, const Point &p);
 
 // -------------------------------------------------------- keccak / merlin
-void keccakf(uint64_t st[25]);
+void keccakf(uint64_t st[25]);          // AVX-512 single-state form when available
+void keccakf_scalar(uint64_t st[25]);   // the portable 64-bit form (reference for the self-test)
+// Framing of a 64-byte TranscriptRng draw that follows another one (STROBE
+// pos 64, pos_begin 0): bytes 64..73 = 0, M|A, 64, 0, 0, 0, 65, I|A|C (the
+// meta_ad of the length and both begin_ops), 71, 0x04 (run_f's pos_begin and
+// padding) and 0x80 at byte 167, as little-endian words 8, 9 and 20.
+static const uint64_t DRAW64_W8 = 0x0741000000401200ULL, DRAW64_W9 = 0x0000000000000447ULL,
+                      DRAW64_W20 = 0x8000000000000000ULL;
+bool have_avx512();
+void keccakf_x1_avx512(uint64_t s[25]);
 void sha3_512(uint8_t out[64], const uint8_t *in, size_t len);
 
 struct Shake256 {
@@ -113,6 +122,7 @@ struct TranscriptRng {
     void rekey_with_witness_bytes(const char *label, const uint8_t *w, size_t n);
     void finalize(const uint8_t entropy[32]);
     void fill_bytes(uint8_t *d, size_t n);
+    void draw64(uint8_t d[64]);   // fill_bytes(d, 64), constant-framing fast path
     Scalar random_scalar() { uint8_t b[64]; fill_bytes(b, 64); return Scalar::from_wide(b); }
 };
 

@@ -422,6 +422,17 @@ Workspace &thread_workspace(int device) {
     BPG_HIP(hipSetDevice(device));
     return *p;
 }
+size_t release_thread_workspace(int device) {
+    auto &m = thread_workspaces();
+    auto it = m.find(device);
+    if (it == m.end() || !it->second) return 0;
+    const size_t b = thread_workspace_bytes(device);
+    BPG_HIP(hipSetDevice(device));
+    BPG_HIP(hipStreamSynchronize(it->second->st));
+    dev::set_prof_sink(nullptr);
+    m.erase(it);
+    return b;
+}
 size_t thread_workspace_bytes(int device) {
     auto &m = thread_workspaces();
     auto it = m.find(device);
@@ -723,6 +734,7 @@ ProducerStage &producer_stage(int device) {
             BPG_HIP(hipHostMalloc((void **)&p->host[b], (size_t)8 * ProducerStage::CHUNK * 64, hipHostMallocDefault));
             BPG_HIP(hipEventCreateWithFlags(&p->ev[b], hipEventBlockingSync | hipEventDisableTiming));
             BPG_HIP(hipEventRecord(p->ev[b], p->st));
+            BPG_HIP(hipEventCreateWithFlags(&p->drawn[b], hipEventDisableTiming));
         }
     }
     BPG_HIP(hipSetDevice(device));
@@ -732,25 +744,37 @@ ProducerStage::~ProducerStage() {
     for (int b = 0; b < 2; b++) {
         if (host[b]) (void)hipHostFree(host[b]);
         if (ev[b]) (void)hipEventDestroy(ev[b]);
+        if (drawn[b]) (void)hipEventDestroy(drawn[b]);
     }
     if (st) (void)hipStreamDestroy(st);
 }
 
 void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
-                    int count, RngBlock *const *out, bool dev_out) {
+                    int count, RngBlock *const *out, bool dev_out, const DrawProgress *progress) {
     if (count < 1 || count > 8) throw std::runtime_error("rng group size");
     Transcript T = prover_transcript(cs, label, label_len);
     TranscriptRng base(T);
     for (uint32_t i = 0; i < cs.m; i++) base.rekey_with_witness_bytes("v_blinding", (const uint8_t *)cs.vb[i].v, 32);
+    // one proof (the latency path): the contiguous single-state STROBE with
+    // its AVX-512 permutation; several: eight states in lockstep (Strobe8)
+    TranscriptRng one(base);
     Strobe8 S;
-    S.from(base.s, count);
-    S.meta_ad((const uint8_t *)"rng", 3);          // TranscriptRngBuilder::finalize
-    S.key_each(entropy, 32);
+    if (count == 1) {
+        one.finalize(entropy[0]);                 // TranscriptRngBuilder::finalize
+    } else {
+        S.from(base.s, count);
+        S.meta_ad((const uint8_t *)"rng", 3);
+        S.key_each(entropy, 32);
+    }
+    auto draw = [&](uint8_t *const *wp) {
+        if (count == 1) one.draw64(wp[0]);
+        else S.draw64(wp);
+    };
     uint8_t tmp[8][64];
     uint8_t *tp[8];
     for (int k = 0; k < 8; k++) tp[k] = tmp[k];
     auto draw_scalars = [&](Scalar RngBlock::*field) {
-        S.draw64(tp);
+        draw(tp);
         for (int k = 0; k < count; k++) out[k]->*field = Scalar::from_wide(tmp[k]);
     };
     draw_scalars(&RngBlock::i_bl);
@@ -762,7 +786,31 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         for (uint64_t i = 0; i < nd; i++) {
             for (int k = 0; k < count; k++) wp[k] = out[k]->wide + 64 * i;
             for (int k = count; k < 8; k++) wp[k] = tmp[k];
-            S.draw64(wp);
+            draw(wp);
+        }
+    } else if (count == 1 && out[0]->stage) {
+        // one proof: draws straight into its pinned buffer, copied up 2 MB at
+        // a time while the next ones are drawn (nothing waits on a copy); the
+        // s_L half ends a chunk, so its copy is the progress point
+        ProducerStage &ps = producer_stage(cs.device);
+        const uint64_t BIG = 32768;
+        uint8_t *h = out[0]->stage;
+        for (int v = 0; v < 2; v++) {
+            const uint64_t a = v ? nd / 2 : 0, b = v ? nd : nd / 2;
+            for (uint64_t i0 = a; i0 < b; i0 += BIG) {
+                const uint64_t len = std::min<uint64_t>(BIG, b - i0);
+                for (uint64_t i = 0; i < len; i++) one.draw64(h + 64 * (i0 + i));
+                BPG_HIP(hipMemcpyAsync(out[0]->wide + 64 * i0, h + 64 * i0, (size_t)len * 64, hipMemcpyHostToDevice,
+                                       ps.st));
+            }
+            if (progress) {
+                BPG_HIP(hipEventRecord(ps.drawn[v], ps.st));
+                (*progress)(v, ps.drawn[v]);
+            }
+        }
+        if (!progress) {
+            BPG_HIP(hipEventRecord(ps.drawn[1], ps.st));
+            event_wait(ps.drawn[1]);
         }
     } else {
         // stream chunks of draws through two pinned staging buffers into
@@ -771,24 +819,34 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         const uint32_t CH = ProducerStage::CHUNK;
         uint8_t *wp[8];
         int buf = 0;
+        bool left_done = false;
         for (uint64_t i0 = 0; i0 < nd; i0 += CH, buf ^= 1) {
             const uint32_t len = (uint32_t)std::min<uint64_t>(CH, nd - i0);
             event_wait(ps.ev[buf]);
             uint8_t *stg = ps.host[buf];
             for (uint32_t i = 0; i < len; i++) {
                 for (int k = 0; k < 8; k++) wp[k] = stg + ((size_t)k * CH + i) * 64;
-                S.draw64(wp);
+                draw(wp);
             }
             for (int k = 0; k < count; k++)
                 BPG_HIP(hipMemcpyAsync(out[k]->wide + 64 * i0, stg + (size_t)k * CH * 64, (size_t)len * 64,
                                        hipMemcpyHostToDevice, ps.st));
             BPG_HIP(hipEventRecord(ps.ev[buf], ps.st));
+            if (progress && !left_done && i0 + len >= nd / 2) {   // all s_L draws are on their way
+                left_done = true;
+                BPG_HIP(hipEventRecord(ps.drawn[0], ps.st));
+                (*progress)(0, ps.drawn[0]);
+            }
+        }
+        if (progress) {
+            BPG_HIP(hipEventRecord(ps.drawn[1], ps.st));
+            (*progress)(1, ps.drawn[1]);
         }
         event_wait(ps.ev[0]);
         event_wait(ps.ev[1]);
     }
     for (int j = 0; j < 5; j++) {
-        S.draw64(tp);
+        draw(tp);
         for (int k = 0; k < count; k++) out[k]->tb[j] = Scalar::from_wide(tmp[k]);
     }
 }
@@ -856,19 +914,58 @@ void rng_draw_multi(const PreparedCS *const *cs, const uint8_t *label, size_t la
     (void)tmp;
 }
 
+// One proof on the calling thread (c_prove, bpg_r1cs_prove, the sharded and
+// prepared single-proof paths). Its latency is the serial TranscriptRng
+// chain (2n + 8 permutations) plus what the device does after it, so the
+// commitment MSMs run under the chain (SURVEY §7 hard part 1): A_I1 / A_O1
+// need no draw and start first, <s_L, G> starts once the s_L half of the
+// draws is on the device (streamed up in chunks as it is drawn) and only
+// <s_R, H> is left when the last draw is made.
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                const uint8_t entropy[32], ProveTimings *tm, const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
+    DeviceContext &ctx = DeviceContext::get(cs.device);
+    std::shared_ptr<const GenSet> gs = ctx.gens(cs.N, cs.rank, cs.world);
     Workspace &ws = thread_workspace(cs.device);
     double t0 = now_ms();
-    ws.stage(2 * (size_t)cs.n * 64 + 64);
+    const uint32_t n = cs.n, nl = cs.nl;
+    ProofBufs &B = ws.pb[0];
+    B.wide.grow(2 * (size_t)n * 64 + 64);
+    B.sL.grow((size_t)nl * sizeof(ScD) + 64);
+    B.sR.grow((size_t)nl * sizeof(ScD) + 64);
+    CommitPre pre;
+    const int64_t gneg = gs->N;
+    PtD *rows = ws.rows_host, *rows_dev = ws.rows_view;
+    if (nl) {
+        const MsmSeg sa[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), gs->G, nl, 0, gneg},
+                              {as<ScD>(const_cast<DBuf &>(cs.aR)), gs->H, nl, 0, gneg},
+                              {as<ScD>(const_cast<DBuf &>(cs.aO)), gs->G, nl, 1, gneg}};
+        int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
+        pre.A = ws.msm->enqueue(sa, 3, 2, rows + CommitPre::ROWS_A, MSM_NIELS, rows_dev + CommitPre::ROWS_A);
+        ws.prof_end(ph);
+    }
+    DrawProgress progress = [&](int v, hipEvent_t drawn) {
+        if (!nl) return;
+        BPG_HIP(hipStreamWaitEvent(ws.st, drawn, 0));
+        ScD *s = as<ScD>(v ? B.sR : B.sL);
+        launch_wide_reduce(as<uint8_t>(B.wide) + (size_t)v * 64 * n, nl, cs.world, cs.rank, s, ws.st);
+        const MsmSeg seg = {s, v ? gs->H : gs->G, nl, 0, gneg};
+        const size_t off = v ? CommitPre::ROWS_S1 : CommitPre::ROWS_S0;
+        int ph = ws.prof_begin("msm_commit", 1.0 * nl * (64 + 32));
+        pre.S[v] = ws.msm->enqueue(&seg, 1, 1, rows + off, MSM_NIELS, rows_dev + off);
+        ws.prof_end(ph);
+    };
+    ws.stage(2 * (size_t)n * 64 + 64);
     RngBlock rb;
-    rb.wide = ws.s_host;
+    rb.wide = as<uint8_t>(B.wide);
+    rb.on_device = true;
+    rb.stage = ws.s_host;
     RngBlock *rbp = &rb;
-    rng_draw_group(cs, label, label_len, &entropy, 1, &rbp, false);
+    rng_draw_group(cs, label, label_len, &entropy, 1, &rbp, true, &progress);
     double t1 = now_ms();
     ProveTimings t;
-    std::vector<uint8_t> pr = gpu_prove_rng(cs, label, label_len, rb, &t, ag);
+    const RngBlock *crb = &rb;
+    std::vector<uint8_t> pr = gpu_prove_lockstep(cs, label, label_len, &crb, 1, &t, ag, &pre)[0];
     t.rng_ms = t1 - t0;
     t.total_ms += t1 - t0;
     last_timings() = t;
@@ -918,7 +1015,7 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // segments (at most 16 per proof, 32 per job).
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms,
-                                                     const AllGather *ag) {
+                                                     const AllGather *ag, const CommitPre *pre) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
     if (P < 1 || P > MAX_LOCKSTEP) throw std::runtime_error("lockstep proof count");
     static_assert(16 * MAX_LOCKSTEP <= MSM_MAX_SEGS, "an IPP job holds up to 16 segments per proof");
@@ -929,6 +1026,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     const bool sharded = world > 1;
     if (sharded && !ag) throw std::runtime_error("sharded prove without an exchange");
     if (sharded && P != 1) throw std::runtime_error("the sharded prover proves one proof at a time");
+    if (pre && P != 1) throw std::runtime_error("precomputed commitments are for one proof");
     std::shared_ptr<const GenSet> gs = ctx.gens(N, rank, world);
     Workspace &ws = thread_workspace(cs.device);
     hipStream_t st = ws.st;
@@ -957,7 +1055,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     // P = 2 and 2^20), leaving HBM for fewer consumers
     const size_t ROWS_PER_PROOF = 192;   // 3 MSMs x at most 64 windows
     MsmPlan pA[MAX_LOCKSTEP] = {};
-    {
+    if (!pre) {
         MsmSeg seg[5 * MAX_LOCKSTEP];
         int nseg = 0;
         for (int p = 0; p < P; p++) {
@@ -995,7 +1093,14 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     for (int p = 0; p < P; p++) {
         const RngBlock &rb = *rbs[p];
         Point AIS[3], tmp;
-        if (nl) {
+        if (nl && pre) {   // A_I1, A_O1 from one job; S1 = <s_L, G> + <s_R, H> from two
+            combine_rows(AIS[0], rowsA + CommitPre::ROWS_A, pre->A.W, pre->A.c);
+            combine_rows(AIS[1], rowsA + CommitPre::ROWS_A + pre->A.W, pre->A.W, pre->A.c);
+            Point sl, sr;
+            combine_rows(sl, rowsA + CommitPre::ROWS_S0, pre->S[0].W, pre->S[0].c);
+            combine_rows(sr, rowsA + CommitPre::ROWS_S1, pre->S[1].W, pre->S[1].c);
+            pt_add(AIS[2], sl, sr);
+        } else if (nl) {
             const MsmPlan &pl = pA[p];
             const PtD *rows = rowsA + ROWS_PER_PROOF * p;
             for (int k = 0; k < 3; k++) combine_rows(AIS[k], rows + k * pl.W, pl.W, pl.c);

@@ -20,6 +20,7 @@
 namespace bpg {
 
 using dev::DBuf;
+using dev::MsmPlan;
 using dev::PtD;
 using dev::ScD;
 
@@ -127,6 +128,8 @@ struct Workspace;
 Workspace &thread_workspace(int device);
 // Device bytes held by the calling thread's workspace on `device` (0: none).
 size_t thread_workspace_bytes(int device);
+// Free the calling thread's workspace on `device` (bpg_ctx_trim); its bytes.
+size_t release_thread_workspace(int device);
 // HBM admission estimates: what a workspace proving P proofs of `cs` in
 // lockstep grows to, and what one Verifier::verify of a circuit of its size
 // needs on a fresh workspace.
@@ -141,6 +144,9 @@ struct RngBlock {
     Scalar tb[5];                // t_1, t_3, t_4, t_5, t_6 blindings
     uint8_t *wide = nullptr;     // 2n x 64 raw bytes: s_L then s_R
     bool on_device = false;      // wide is a device buffer (batched path)
+    // single proof with a device `wide`: a pinned host buffer of all 2n draws,
+    // copied up in large chunks as they are drawn (no staging round trips)
+    uint8_t *stage = nullptr;
 };
 // Per-thread staging of RNG output into device buffers.
 struct ProducerStage {
@@ -148,13 +154,18 @@ struct ProducerStage {
     hipStream_t st = nullptr;                 // this producer thread's copy stream
     uint8_t *host[2] = {nullptr, nullptr};   // pinned, 8 x CHUNK x 64 B each
     hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t drawn[2] = {nullptr, nullptr};   // s_L / s_R copies complete (rng_draw_group's progress)
     ~ProducerStage();
 };
 ProducerStage &producer_stage(int device);
 // Draw the RNG streams of `count` (<= 8) proofs of `cs` in lockstep. With
-// dev_out the s_L | s_R draws go to out[k]->wide as device buffers.
+// dev_out the s_L | s_R draws go to out[k]->wide as device buffers, and
+// `progress(v, ev)` (if given, dev_out only) is called once all s_L (v = 0)
+// and once all s_R (v = 1) draws have been copied up: `ev` completes when
+// the copies have landed (a stream that waits on it may read them).
+typedef std::function<void(int, hipEvent_t)> DrawProgress;
 void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *const *entropy,
-                    int count, RngBlock *const *out, bool dev_out);
+                    int count, RngBlock *const *out, bool dev_out, const DrawProgress *progress = nullptr);
 // The same for up to 8 proofs of DIFFERENT prepared statements (lockstep
 // after each statement's first draw); wide draws go to device buffers.
 void rng_draw_multi(const PreparedCS *const *cs, const uint8_t *label, size_t label_len,
@@ -171,12 +182,22 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
 // partial sums; all ranks return the same proof bytes.
 std::vector<uint8_t> gpu_prove_rng(const PreparedCS &cs, const uint8_t *label, size_t label_len, const RngBlock &rb,
                                    ProveTimings *tm = nullptr, const AllGather *ag = nullptr);
-// The same for P (<= 2) proofs of one circuit in lockstep on the calling
-// thread's stream (one MSM job per step for all of them); tms: P entries or
-// null. P must be 1 when sharded.
+// Commitment MSMs of a single proof enqueued while its TranscriptRng was
+// still being drawn (gpu_prove): A_I1 / A_O1 (no RNG input) before the
+// draws, <s_L, G> and <s_R, H> as soon as each half is on the device. Window
+// rows in the calling thread's pinned row buffer at the offsets below.
+struct CommitPre {
+    MsmPlan A, S[2];
+    static const size_t ROWS_A = 0, ROWS_S0 = 256, ROWS_S1 = 384;
+};
+// The same for P (<= MAX_LOCKSTEP = 4) proofs of one circuit in lockstep on
+// the calling thread's stream (one MSM job per IPP step for all of them);
+// tms: P entries or null. P must be 1 when sharded. pre: P = 1 and the
+// commitment jobs already enqueued on this thread's stream (s_L, s_R reduced
+// into its proof buffers).
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms = nullptr,
-                                                     const AllGather *ag = nullptr);
+                                                     const AllGather *ag = nullptr, const CommitPre *pre = nullptr);
 // Verifier::verify; returns 1 accept / 0 reject.
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                const uint8_t *proof, size_t proof_len, const uint8_t entropy[32]);

@@ -38,6 +38,8 @@ struct Strobe8 {
 };
 
 void keccak8(uint64_t L[25][8]);
+// Keccak-f[1600] of one state with AVX-512 (call only when have_avx512())
+void keccakf_x1_avx512(uint64_t s[25]);
 bool have_avx512();
 
 }  // namespace bpg

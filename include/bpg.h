@@ -201,9 +201,10 @@ int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes);
  * allocating the tables' memory, out[4] bytes of comb tables resident. */
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n);
 /* Release the device's cached comb tables and sharded generator slices that
- * no proof in flight holds (they are rebuilt on next use): lets another
- * process or circuit size on the same GPU have the HBM. Returns the bytes of
- * comb tables released, < 0 on error. */
+ * no proof in flight holds, and the batch worker pool's (and the caller's)
+ * per-thread device workspaces (they are rebuilt on next use): lets another
+ * process or circuit size on the same GPU have the HBM. Call it between
+ * batches. Returns the bytes released, < 0 on error. */
 int64_t bpg_ctx_trim(bpg_ctx *ctx);
 
 /* Ensure G_i, H_i for i < capacity are resident (BulletproofGens::new(cap,1),

@@ -218,7 +218,8 @@ def test_batch_layouts_bit_exact(bpg, resources, producers, lockstep):
     ents = [bytes([k + 40]) * 32 for k in range(11)]
     proofs = prep.prove_batch(b"layout", ents, threads=producers + 3)
     st = bpg.last_batch_stats()
-    assert st["producers"] == producers and st["lockstep"] == lockstep and st["consumers"] >= 1
+    # 11 proofs are two RNG groups of 8: at most two producers have work
+    assert st["producers"] == min(producers, 2) and st["lockstep"] == lockstep and st["consumers"] >= 1
     assert st["wall_ms"] > 0 and st["producer_draw_ms"] > 0 and st["consumer_prove_ms"] > 0
     for k in (0, 5, 10):
         assert proofs[k] == c.r1cs_prove(b"layout", syn.view, ents[k])[0]

@@ -92,6 +92,53 @@ def test_synthesis_errors_are_reported(bpg, bad):
         bpg.Synth(*bad)
 
 
+def _kernel_resources():
+    """Per-kernel register report of the gfx950 build (the Makefile compiles
+    kernels.hip with -Rpass-analysis=kernel-resource-usage)."""
+    path = os.path.join(ROOT, "bulletproof-gadgets_amd", "build", "kernels.resources")
+    if not os.path.exists(path):
+        pytest.skip("kernels.hip not built in-tree")
+    rows, cur = {}, None
+    for line in open(path):
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = rows.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z \[\]/]+): (\S+) \[", line)
+        if m and cur is not None:
+            cur[m.group(1).strip()] = m.group(2)
+    return rows
+
+
+@pytest.mark.parametrize("mangled,waves", [
+    ("k_rbk_passILb1ELi1ELb1E", 3),     # MSM pass 1 over the generators (the dominant kernel)
+    ("k_rbk_passILb1ELi0ELb0E", 2),     # MSM pass 1 over folded (cached) bases
+    ("k_rbk_passILb0ELi0ELb0E", 1),     # run merges
+    ("k_ipp_comb_fold", 2),
+    ("k_ipp_fold3I3gecE", 1),
+    ("k_row_reduce", 1),
+    ("k_rs_scatterILi8ELb1E", 3),
+])
+def test_hot_kernels_do_not_spill(mangled, waves):
+    """The hot kernels keep their registers: no VGPR spills, no scratch, and
+    at least the occupancy each is designed for (a restructured loop once
+    made pass 1 spill 56 VGPRs to scratch)."""
+    rows = _kernel_resources()
+    hits = [v for k, v in rows.items() if mangled in k]
+    assert hits, mangled
+    for r in hits:
+        assert r["VGPRs Spill"] == "0" and r["ScratchSize [bytes/lane]"] == "0", r
+        assert int(r["Occupancy [waves/SIMD]"]) >= waves, r
+
+
+def test_rng_selftest(bpg):
+    """Host RNG (no device): the AVX-512 single-state and eight-state Keccak-f
+    permutations equal the portable scalar one, TranscriptRng's 64-byte
+    draw fast path equals fill_bytes, and the lockstep Strobe8 lanes equal
+    independent TranscriptRngs (bpg_rng_selftest: 0 = all equal)."""
+    assert bpg.lib().bpg_rng_selftest() == 0
+
+
 def test_product_fails_loudly_without_device(bpg, resources):
     if os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES") != "":
         pytest.skip("a HIP device may be present")
