@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fold-tables", type=int, default=-1, choices=(-1, 0, 1),
                     help="IPP comb tables: 1 on, 0 off (the path a device without ~208 GB free takes), -1 default")
+    ap.add_argument("--msm-tables", type=int, default=-1, choices=(-1, 0, 1),
+                    help="fixed-base generator tables for the MSMs over the generators (13 windows of 20 bits, "
+                         "~7 GB at 2^20): 1 on, 0 off, -1 default (on where they fit)")
     ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification); latency: one proof at a time, sharded over all "
@@ -360,8 +363,8 @@ def main():
     bpg.set_seed(1000 + srank)
     syn = bpg.Synth(inst, wit, gad)
     ctx = bpg.Context(dev)
-    if a.fold_tables >= 0:
-        ctx.set_strategy(fold_tables=a.fold_tables)
+    if a.fold_tables >= 0 or a.msm_tables >= 0:
+        ctx.set_strategy(fold_tables=a.fold_tables, msm_tables=a.msm_tables)
     ctx.set_pipeline(producers=min(producers, 8))
     if a.mode == "latency":
         return bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W)
@@ -506,7 +509,8 @@ def main():
                    "proofs_per_step_per_gpu": batch, "host_threads_per_gpu": threads,
                    "parallelism": "independent proofs per GPU (%d ranks)" % world,
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
-                   "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables]},
+                   "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables],
+                   "msm_fixed_base_tables": {-1: "default (on where they fit)", 0: "off", 1: "on"}[a.msm_tables]},
         "host_cores_busy": round(host_busy, 2),
         # the producer/consumer pipeline of the timed batch (bpg_last_batch_stats):
         # consumer time starved of ready proofs while producers were drawing
@@ -515,6 +519,7 @@ def main():
         "hbm_used_gb": round((total_b - free_b) / 1e9, 1),
         "latency_ms_single_proof": round(single_ms, 1),
         "cold_setup_ms": round(prepare_ms, 1),
+        "msm_table_gb": round(ctx.setup_stats()["msm_table_bytes"] / 1e9, 2),
         "cold_setup_breakdown_ms": {"generators": round(setup["gens_ms"], 1), "comb_tables": round(setup["comb_ms"], 1),
                                     "comb_tables_alloc": round(setup["comb_alloc_ms"], 1),
                                     "generators_from_disk_cache": setup["gens_from_cache"]},

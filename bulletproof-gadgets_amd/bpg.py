@@ -32,7 +32,7 @@ EXPORTS = [
     "bpg_cs_commit", "bpg_cs_commit_point", "bpg_cs_multiply", "bpg_cs_allocate_multiplier", "bpg_cs_constrain",
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
     "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim", "bpg_prove_statements",
-    "bpg_ctx_set_pipeline", "bpg_last_batch_stats", "bpg_last_statements_stats",
+    "bpg_ctx_set_pipeline", "bpg_last_batch_stats", "bpg_last_statements_stats", "bpg_ctx_set_msm_tables",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -95,6 +95,7 @@ def lib():
         L.bpg_ctx_set_ipp_tail.argtypes = [vp, ctypes.c_int]
         L.bpg_ctx_setup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_ctx_set_pipeline.argtypes = [vp, u32, u32, u32]
+        L.bpg_ctx_set_msm_tables.argtypes = [vp, ctypes.c_int]
         L.bpg_last_batch_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_last_statements_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_r1cs_prove_sharded.argtypes = [vp, vp, sz, vp, vp, u32, u32, ALLGATHER_FN, vp, vp, sz,
@@ -365,12 +366,14 @@ class Context:
         if not self.h:
             raise BpgError(last_error())
 
-    def set_strategy(self, fold_tables=-1, fold_pairs=-1, ipp_tail=-1):
+    def set_strategy(self, fold_tables=-1, fold_pairs=-1, ipp_tail=-1, msm_tables=-1):
         """IPP fold strategy of this context's calls (bpg_ctx_set_fold_*,
-        bpg_ctx_set_ipp_tail); fold_pairs 2 folds rounds in triples."""
+        bpg_ctx_set_ipp_tail); fold_pairs 2 folds rounds in triples;
+        msm_tables: fixed-base generator tables (bpg_ctx_set_msm_tables)."""
         if lib().bpg_ctx_set_fold_tables(self.h, fold_tables) != 0 or \
                 lib().bpg_ctx_set_fold_pairs(self.h, fold_pairs) != 0 or \
-                lib().bpg_ctx_set_ipp_tail(self.h, ipp_tail) != 0:
+                lib().bpg_ctx_set_ipp_tail(self.h, ipp_tail) != 0 or \
+                lib().bpg_ctx_set_msm_tables(self.h, msm_tables) != 0:
             raise BpgError("bad strategy")
 
     def set_pipeline(self, producers=0, lockstep=0, max_inflight=0):
@@ -380,10 +383,10 @@ class Context:
             raise BpgError("bad pipeline layout")
 
     def setup_stats(self):
-        arr = (ctypes.c_double * 5)()
-        lib().bpg_ctx_setup_stats(self.h, arr, 5)
+        arr = (ctypes.c_double * 6)()
+        lib().bpg_ctx_setup_stats(self.h, arr, 6)
         return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2]), "comb_alloc_ms": arr[3],
-                "comb_bytes": arr[4]}
+                "comb_bytes": arr[4], "msm_table_bytes": arr[5]}
 
     def trim(self):
         """bpg_ctx_trim: drop cached comb tables / generator slices no proof

@@ -76,7 +76,18 @@ struct MsmSeg {
     // (0: no such copy). When every segment of a Niels job has one, a
     // negative digit gathers the negated base instead of negating it.
     int64_t negofs = 0;
+    // fixed-base job (every segment of a Niels job sets it): the bases are
+    // generator tables, window w's multiple 2^(FB_C w) P_i at base + w
+    // wstride + i (and its negation at + negofs); digits of all FB_W windows
+    // go to one bucket row per MSM (0: an ordinary job)
+    uint64_t wstride = 0;
 };
+// Fixed-base generator tables (DESIGN.md "Fixed-base windows"): 20-bit
+// signed windows, 13 of them cover a canonical scalar.
+static const int FB_C = 20, FB_W = 13;
+// tab[w * 2N + i] = 2^(FB_C w) gens[i], tab[w * 2N + N + i] its negation,
+// w < FB_W (affine Niels)
+void launch_fb_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st);
 struct MsmPlan {
     int c, W, nmsm, rows, half;   // W: digit windows per scalar = rows per MSM
     uint64_t total;         // points in the job

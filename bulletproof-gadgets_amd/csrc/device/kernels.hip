@@ -267,12 +267,15 @@ DEVI int seg_of(const uint32_t *gofs, int n, uint32_t g) {
 struct TileGeo {
     uint32_t nt, rows, tile, TW;      // tiles, rows, entries per tile, tiles per window
     uint32_t moff[TILEGEO_MAXMSM], mtot[TILEGEO_MAXMSM], tpr[TILEGEO_MAXMSM], cum[TILEGEO_MAXMSM];
+    // fixed-base jobs: MSM m's points [pmoff[m], pmoff[m] + pmtot[m]); its
+    // one row holds their W windows' entries [w][point] from W pmoff[m]
+    uint32_t pmoff[TILEGEO_MAXMSM], pmtot[TILEGEO_MAXMSM];
     uint8_t *bflag;                   // cleared: bflag_bytes (multiple of 16)
     uint64_t bflag_bytes;
     uint32_t *tiles;                  // null: the host wrote the table
 };
 __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
-                             uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G) {
+                             uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G, uint32_t wstride) {
     WAVE_PRIO(BPG_SORT_PRIO);
     __shared__ uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -315,8 +318,10 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
         if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
         uint32_t d = (uint32_t)(x >> sh) & mask;
         d += carry;
-        const uint32_t row = (uint32_t)w * nmsm + m;
-        uint32_t slot = half, val = loc;
+        // rows window-major (row = w nmsm + m), or one per MSM for a
+        // fixed-base job, whose entry of window w gathers table w
+        const uint32_t row = wstride ? m : (uint32_t)w * nmsm + m;
+        uint32_t slot = half, val = wstride ? loc + (uint32_t)w * wstride : loc;
         if (d > half) {
             uint32_t mag = full - d;
             carry = 1;
@@ -325,8 +330,10 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
             carry = 0;
             if (d) slot = d - 1;
         }
-        // rows contiguous: [w][g], one row per window and MSM
-        const size_t pos = (size_t)w * total + g;
+        // rows contiguous: [w][g], one row per window and MSM; fixed-base:
+        // [m][w][point of m]
+        const size_t pos = wstride ? (size_t)W * G.pmoff[m] + (size_t)w * G.pmtot[m] + (g - G.pmoff[m])
+                                   : (size_t)w * total + g;
         keys[pos] = row << c | slot;
         vals[pos] = val;
     }
@@ -660,6 +667,7 @@ __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? RBK_LAT_WAVES : FMT == MSM_CACH
     };
     if constexpr (FIRST) {
         typedef typename BaseOf<FMT>::T BT;
+        typedef typename BaseOf<FMT>::T BT;
         BT pa;
         const uint32_t *skt = sk + rbk_lds(t * RBK_T), *svt = sv + rbk_lds(t * RBK_T);   // chunk has no pad inside
         if (!rbk_trash(first, cw)) msm_load_base<FMT, NEGC>(pa, sptr, svt[0]);
@@ -751,7 +759,7 @@ DEVI void bucket_load(ge &p, const ge *__restrict__ B, const uint8_t *__restrict
 // kernels of other streams for up to a millisecond, so every register they do
 // not need is room for another wave of those (ROW_WAVES / BSEG_WAVES: waves
 // per SIMD compiled for).
-static constexpr int BSEG_WAVES = 3, ROW_WAVES = 1;
+static constexpr int BSEG_WAVES = 3, ROW_WAVES = 2;
 __global__ __launch_bounds__(64, BSEG_WAVES) void k_bucket_seg(const ge *__restrict__ buckets, const uint8_t *__restrict__ bflag,
                                                    uint32_t rows, uint32_t half, uint32_t seglen, uint32_t nseg,
                                                    ge *__restrict__ segA, ge *__restrict__ segT) {
@@ -775,14 +783,43 @@ DEVI void ge_dbl_n(ge &r, int n) {
     for (int i = 1; i < n; i++) ge_dbl_t<false>(r, r);
     if (n > 0) ge_dbl_t<true>(r, r);
 }
+// p + q with q read from memory (global or LDS) one coordinate at a time,
+// right before its products: 10 live registers for q instead of 40 (ge_add's
+// formula and bounds)
+DEVI void ge_add_mem(ge &r, const ge &p, const ge *q) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(q);
+    fe a, b, c, d, u, v;
+#pragma unroll
+    for (int k = 0; k < 10; k++) { u.v[k] = w[10 + k]; v.v[k] = w[k]; }   // q.Y, q.X
+    fe t;
+    fe_sub_nc(t, u, v);                                   // 3T
+    fe_add_nc(v, u, v);                                   // 2T
+    fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, t);
+    fe_add_nc(b, p.Y, p.X); fe_mul(b, b, v);
+#pragma unroll
+    for (int k = 0; k < 10; k++) u.v[k] = w[30 + k];      // q.T
+    fe_mul(c, p.T, u); fe_mul(c, c, FE_D2);
+#pragma unroll
+    for (int k = 0; k < 10; k++) u.v[k] = w[20 + k];      // q.Z
+    fe_add_nc(u, u, u); fe_mul(d, p.Z, u);
+    fe e, f, g, h;
+    fe_sub_nc(e, b, a); fe_sub_nc(f, d, c); fe_add_nc(g, d, c); fe_add_nc(h, b, a);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+}
 // Level 2, one block per row; thread t owns segments [tK, tK + K):
 //   sum_s s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t,
 //   sum_t t run_t = sum_{k>=1} suffix_k (suffix scan in LDS).
 // The row is sum A_s + L * (that). L and K are powers of two.
 // Rows are numbered window-major (row = w * nmsm + msm); results land at
 // msm * W + w, the layout the host combine reads.
+// Registers: every second operand is read from memory coordinate by
+// coordinate (ge_add_mem), and acc / run wait out the LDS scan in the
+// thread's own (consumed) segT slots, so at most two points are live: the
+// kernel then fits on a SIMD next to two waves of MSM pass 1 (it held 225
+// registers, and under the bench's concurrency waited ~10x its isolated time
+// for a SIMD with that much room, profiles/r03w_pmc_table.md).
 DEVI uint32_t row_perm(uint32_t row, uint32_t nmsm, uint32_t W) { return (row % nmsm) * W + row / nmsm; }
-__global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restrict__ segA, const ge *__restrict__ segT,
+__global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restrict__ segA, ge *__restrict__ segT,
                                                     uint32_t nseg, int lgL, uint32_t nmsm, uint32_t W,
                                                     ge *__restrict__ rows_out) {
     __shared__ ge sh[256];
@@ -791,23 +828,31 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
     const uint32_t K = (nseg + 255) / 256;
     int lgK = 0;
     while ((1u << lgK) < K) lgK++;
-    const ge *A = segA + (size_t)row * nseg, *T = segT + (size_t)row * nseg;
+    const ge *A = segA + (size_t)row * nseg;
+    ge *T = segT + (size_t)row * nseg;
     // sum_s A_s is added at the end (three points live at most, not four)
-    ge run, acc, p;
+    ge run, acc;
     ge_identity(run); ge_identity(acc);
     for (int k = (int)K - 1; k >= 0; k--) {
         uint32_t s = t * K + k;
         if (s >= nseg) continue;
-        ge_load(p, T + s); ge_add(run, run, p);
+        ge_add_mem(run, run, T + s);
         ge_add(acc, acc, run);
     }
+    // run and acc wait out the scan in this thread's first two segT slots
+    // (their T_s are consumed); with one segment acc = run, with none both
+    // are the identity
+    const uint32_t s0 = t * K;
+    const bool has = s0 < nseg, two = has && s0 + 1 < nseg;
+    if (has) ge_store(T + s0, run);
+    if (two) ge_store(T + s0 + 1, acc);
     // inclusive suffix scan of run over threads
     ge_store(&sh[t], run);
     for (uint32_t d = 1; d < 256; d <<= 1) {
         __syncthreads();
-        ge a, b;
+        ge a;
         const bool act = t + d < 256;
-        if (act) { ge_load(a, &sh[t]); ge_load(b, &sh[t + d]); ge_add(a, a, b); }
+        if (act) { ge_load(a, &sh[t]); ge_add_mem(a, a, &sh[t + d]); }
         __syncthreads();
         if (act) ge_store(&sh[t], a);
     }
@@ -816,22 +861,24 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
     ge_load(suf, &sh[t]);
     if (t == 0) ge_identity(suf);
     ge_dbl_n(suf, lgK);                    // K * suffix_t
+    if (has) ge_load(run, T + s0); else ge_identity(run);
+    if (two) ge_load(acc, T + s0 + 1); else acc = run;
     ge_sub(q, acc, run);
     ge_add(q, q, suf);
     ge_dbl_n(q, lgL);                      // L * (...)
     for (uint32_t k = 0; k < K; k++) {     // + this thread's A_s
         uint32_t s = t * K + k;
         if (s >= nseg) break;
-        ge_load(p, A + s); ge_add(q, q, p);
+        ge_add_mem(q, q, A + s);
     }
     __syncthreads();
     ge_store(&sh[t], q);
     for (int w = 128; w >= 1; w >>= 1) {
         __syncthreads();
         if (t < (uint32_t)w) {
-            ge a, b;
-            ge_load(a, &sh[t]); ge_load(b, &sh[t + w]);
-            ge_add(a, a, b);
+            ge a;
+            ge_load(a, &sh[t]);
+            ge_add_mem(a, a, &sh[t + w]);
             ge_store(&sh[t], a);
         }
     }
@@ -970,8 +1017,18 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     if (total > 0x7fffffffu) throw HipError(hipErrorInvalidValue, "msm job too large", __FILE__, __LINE__);
     T.gofs[nseg] = (uint32_t)total;
     p.total = total;
-    p.c = msm_window(total, nmsm, fmt);
-    p.W = (254 + p.c - 1) / p.c;
+    // fixed-base job: every segment gathers from generator tables (wstride):
+    // FB_C-bit windows, all of a point's windows in its MSM's one row
+    const uint64_t wstride = segs[0].wstride;
+    const bool fb = wstride != 0;
+    for (int i = 0; i < nseg; i++)
+        if (segs[i].wstride != wstride) throw HipError(hipErrorInvalidValue, "mixed fixed-base job", __FILE__, __LINE__);
+    if (fb && (fmt != MSM_NIELS || nmsm > TILEGEO_MAXMSM))
+        throw HipError(hipErrorInvalidValue, "fixed-base job", __FILE__, __LINE__);
+    p.c = fb ? FB_C : msm_window(total, nmsm, fmt);
+    const int Wd = (254 + p.c - 1) / p.c;   // digit windows
+    if (fb && Wd != FB_W) throw HipError(hipErrorInvalidValue, "fixed-base windows", __FILE__, __LINE__);
+    p.W = fb ? 1 : Wd;                       // window rows per MSM (what the host combines)
     p.nmsm = nmsm;
     p.rows = nmsm * p.W;
     p.half = 1 << (p.c - 1);
@@ -990,7 +1047,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     bool negc = fmt == MSM_NIELS;
     const size_t psz = fmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
     for (int i = 0; i < nseg; i++) {
-        if (segs[i].count > MSM_LOC_MASK) throw HipError(hipErrorInvalidValue, "msm segment too large", __FILE__, __LINE__);
+        if (segs[i].count > MSM_LOC_MASK || (fb && (uint64_t)(Wd - 1) * wstride + segs[i].count > MSM_LOC_MASK))
+            throw HipError(hipErrorInvalidValue, "msm segment too large", __FILE__, __LINE__);
         T.scal[i] = AS_CSC(segs[i].scal);
         T.base[i] = segs[i].base;
         T.neg[i] = segs[i].negofs ? (const void *)((const uint8_t *)segs[i].base + segs[i].negofs * (int64_t)psz)
@@ -998,7 +1056,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         negc = negc && segs[i].negofs != 0;
         T.row0[i] = segs[i].msm;
     }
-    p.E0 = (uint64_t)p.W * total;
+    p.E0 = (uint64_t)Wd * total;
     p.T = RBK_T;
     // keys: row << c | slot (slot <= half, half = trash); padding key = rows << c
     const uint64_t D = (uint64_t)p.rows * p.half;
@@ -1009,8 +1067,9 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     // buckets per first-level segment (k_bucket_seg): a row of `half`
     // buckets leaves half / seglen segments for the one-block row reduction,
     // whose serial part is 3 additions per segment per thread (16 or 32
-    // measured 0.5-2% slower, profiles/r03j_ab_tskip_seglen.txt)
-    const uint32_t seg_cfg = 8;
+    // measured 0.5-2% slower, profiles/r03j_ab_tskip_seglen.txt); the 2^19
+    // buckets of a fixed-base row take 64 per segment (8192 segments)
+    const uint32_t seg_cfg = std::max<uint32_t>(8, (uint32_t)p.half / 8192);
     p.seglen = p.half < seg_cfg ? p.half : seg_cfg;
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
@@ -1033,10 +1092,15 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     geo.bflag_bytes = (D + 15) / 16 * 16;   // bflag_ holds D + D/4 + 256 bytes
     uint32_t nt = 0;
     if (nmsm <= TILEGEO_MAXMSM) {   // the digit launch writes the tile table
+        // (a fixed-base job is tiled as one window whose MSM m holds Wd
+        // entries per point)
+        const uint32_t scale = fb ? (uint32_t)Wd : 1u;
         for (int m = 0; m < nmsm; m++) {
-            geo.moff[m] = moff[m];
-            geo.mtot[m] = mtot[m];
-            geo.tpr[m] = (uint32_t)((mtot[m] + tile - 1) / tile);
+            geo.moff[m] = scale * moff[m];
+            geo.mtot[m] = scale * mtot[m];
+            geo.pmoff[m] = moff[m];
+            geo.pmtot[m] = mtot[m];
+            geo.tpr[m] = (uint32_t)((geo.mtot[m] + tile - 1) / tile);
             geo.cum[m] = geo.TW;
             geo.TW += geo.tpr[m];
         }
@@ -1074,8 +1138,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     }
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     ge *buckets = AS_GE(buckets_.p);
-    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, p.W,
-                       (uint32_t)nmsm, (uint32_t)p.half, keys, vals, geo);
+    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, Wd,
+                       (uint32_t)nmsm, (uint32_t)p.half, keys, vals, geo, (uint32_t)wstride);
     BPG_HIP(hipGetLastError());
     radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
@@ -1127,7 +1191,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
                        (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, segA, segT);
     int lgL = 0;
     while ((1 << lgL) < p.seglen) lgL++;
-    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, (const ge *)segT,
+    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, segT,
                        (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out));
     BPG_HIP(hipGetLastError());
     if (!rows_direct)
@@ -1889,9 +1953,37 @@ DEVI void foldn_get(gec &c, const uint32_t *tb) {
 #pragma unroll
     for (int k = 0; k < 40; k++) w[k] = tb[k * 64];
 }
+#ifndef FOLD3_LAZY
+#define FOLD3_LAZY 0
+#endif
 // waves per SIMD the triple fold is compiled for (332 VGPRs; at 2 waves
 // it spilled and measured slower, profiles/r03c_ab_commitjob_fold3_smallmsm.txt)
-static constexpr int FOLD3_WAVES = 1;
+static constexpr int FOLD3_WAVES = FOLD3_LAZY ? 2 : 1;
+// one coordinate of a table entry (word-major, lane stride 64)
+DEVI void foldn_get_fe(fe &x, const uint32_t *tb) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) x.v[k] = tb[k * 64];
+}
+// acc + (SUB: -) the cached point of table entry `e`, each coordinate loaded
+// right before its product: 10 live registers for the operand, not 40
+template <bool SUB>
+DEVI void ge_addsub_tab(ge &r, const ge &p, const uint32_t *e) {
+    fe a, b, c, d, q;
+    foldn_get_fe(q, e + (SUB ? 0 : 10) * 64);   // Y-X (Y+X for -P)
+    fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q);
+    foldn_get_fe(q, e + (SUB ? 10 : 0) * 64);   // Y+X (Y-X for -P)
+    fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q);
+    foldn_get_fe(q, e + 30 * 64);                // 2dT
+    fe_mul(c, p.T, q);
+    foldn_get_fe(q, e + 20 * 64);                // 2Z
+    fe_mul(d, p.Z, q);
+    fe ee, f, g, h;
+    fe_sub_nc(ee, b, a);
+    if (SUB) { fe_add_nc(f, d, c); fe_sub_nc(g, d, c); }
+    else { fe_sub_nc(f, d, c); fe_add_nc(g, d, c); }
+    fe_add_nc(h, b, a);
+    fe_mul(r.X, ee, f); fe_mul(r.Y, g, h); fe_mul(r.T, ee, h); fe_mul(r.Z, f, g);
+}
 // the lane's odd multiples P, 3P, .. of the seven points into the block's
 // word-major table
 template <class P>
@@ -1936,6 +2028,18 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
+#if FOLD3_LAZY
+    for (uint32_t k = 1; k < nops; k++) {
+        const uint32_t op = fold2_op(ops, k);
+        const uint32_t g = op & 255;
+        if (g) {
+            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
+            ge_dbl_t<true>(acc, acc);
+        }
+        const uint32_t *e = foldn_entry(tb, op);
+        if (op >> 15) ge_addsub_tab<true>(acc, acc, e); else ge_addsub_tab<false>(acc, acc, e);
+    }
+#else
     // the next op's table entry is loaded before the doublings
     gec c;
     if (nops > 1) foldn_get(c, foldn_entry(tb, fold2_op(ops, 1)));
@@ -1954,6 +2058,7 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
         c = cn;
     }
+#endif
     const uint32_t tail = A.tail[sg];
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);
@@ -2458,6 +2563,32 @@ __global__ __launch_bounds__(64) void k_niels_neg(const gen *__restrict__ in, ge
     gen_load(p, in + j);
     gen_cneg(p, true);
     gen_store(out + j, p);
+}
+// Fixed-base tables: one generator per lane, window w = 2^(FB_C w) P by
+// FB_C doublings from window w - 1, made affine (one inversion each: a
+// one-time build, ~2 ms for both 2^20 vectors)
+__global__ __launch_bounds__(64) void k_fb_build(const gen *__restrict__ gens, uint32_t N, gen *__restrict__ tab) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const size_t S = 2 * (size_t)N;
+    gen g, e;
+    gen_load(g, gens + i);
+    gen_store(tab + i, g);
+    e = g; gen_cneg(e, true); gen_store(tab + N + i, e);
+    ge p;
+    ge_from_niels(p, g);   // (2X : 2Y : 2 : 2T)
+    for (int w = 1; w < FB_W; w++) {
+        for (int k = 0; k < FB_C; k++) ge_dbl_t<false>(p, p);
+        ge_to_niels(e, p);
+        gen_store(tab + w * S + i, e);
+        gen_cneg(e, true);
+        gen_store(tab + w * S + N + i, e);
+    }
+}
+void launch_fb_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st) {
+    if (!N) return;
+    hipLaunchKernelGGL(k_fb_build, dim3(nblk(N, 64)), dim3(64), 0, st, AS_CGEN(gens), N, AS_GEN(tab));
+    BPG_HIP(hipGetLastError());
 }
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st) {
     if (!count) return;

@@ -164,6 +164,11 @@ int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode) {
     ctx->strat.fold_pairs = mode;
     return 0;
 }
+int bpg_ctx_set_msm_tables(bpg_ctx *ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) return -1;
+    ctx->strat.msm_tables = mode;
+    return 0;
+}
 int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes) {
     if (!ctx || lanes < -1) return -1;
     ctx->strat.ipp_tail = lanes;
@@ -178,10 +183,11 @@ int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
     if (!ctx) return -1;
     DeviceContext &c = DeviceContext::get(ctx->device);
     std::lock_guard<std::mutex> lk(c.mu);
-    double resident = 0;
+    double resident = 0, fb = 0;
     for (auto &e : c.combs) resident += (double)e.second->bytes;
-    const double v[5] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms, resident};
-    for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+    for (auto &e : c.fbs) fb += (double)e.second->bytes;
+    const double v[6] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms, resident, fb};
+    for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
     return 0;
 }
 int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity) {
@@ -397,6 +403,10 @@ int64_t bpg_ctx_trim(bpg_ctx *ctx) {
             }
             for (auto e = c.slices.begin(); e != c.slices.end();) {
                 if (e->second.use_count() == 1) e = c.slices.erase(e);
+                else ++e;
+            }
+            for (auto e = c.fbs.begin(); e != c.fbs.end();) {
+                if (e->second.use_count() == 1) { freed += (int64_t)e->second->bytes; e = c.fbs.erase(e); }
                 else ++e;
             }
         }
@@ -702,10 +712,14 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         std::vector<std::unique_ptr<PreparedCS>> spare;
         uint32_t next = 0, synth_busy = 0, inflight = 0, done = 0, proved = 0;
         // statements in flight (synthesised, prepared, drawn or being proved):
-        // at most W + 8 + 2C, and at most what HBM holds next to the
-        // consumers' workspaces, sized once the first statement is prepared
-        // (until then at most W)
-        uint32_t limit = W + 8 + 2 * C, hbm_limit = 0;
+        // a statement spends ~0.5 s between its synthesis and the end of its
+        // RNG group's draw (the group forms from eight prepared statements),
+        // so by Little's law the in-flight count bounds the rate: W + 8 + 2C
+        // (40 at 16 workers) held it to ~35 statements/s
+        // (profiles/r04d_statements.json). At most 4W + 8 + 2C, and at most
+        // what HBM holds next to the consumers' workspaces, sized once the
+        // first statement is prepared (until then at most W)
+        uint32_t limit = 4 * W + 8 + 2 * C, hbm_limit = 0;
         double est_st = 0;
         double synth_ms = 0, prep_ms = 0, rng_ms = 0, prove_ms = 0, widle_ms = 0, cidle_ms = 0;
         std::string first_err;

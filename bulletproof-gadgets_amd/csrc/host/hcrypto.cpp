@@ -3,6 +3,8 @@
 // transcript.rs), FIPS 202 Keccak, RFC 8439 ChaCha20.
 #include "hcrypto.h"
 
+#include <chrono>
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <sys/random.h>
@@ -479,10 +481,26 @@ void keccakf_scalar(uint64_t s[25]) {
     s[20] = a20; s[21] = a21; s[22] = a22; s[23] = a23; s[24] = a24;
 }
 #undef ROL
-// AVX-512 single-state permutation where the CPU has it (rng8.cpp:
-// keccakf_x1_avx512, ~1.6-2x the scalar speed); the scalar form otherwise
+// One state: the AVX-512 form or the scalar one, whichever is faster on
+// this CPU, measured once (the single-proof TranscriptRng chain is ~1.5 M
+// serial permutations). The two differ by CPU: on the Intel host of the
+// build container the AVX-512 form takes 464 vs 690 ns, on the GPU box's
+// EPYC 9575F 244 vs 191 ns (profiles/r04d_rng_bench.txt).
+static bool pick_avx512_x1() {
+    if (!have_avx512()) return false;
+    uint64_t a[25] = {1}, b[25] = {1};
+    auto time = [](void (*f)(uint64_t *), uint64_t *st) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < 4000; i++) f(st);
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    };
+    time(keccakf_scalar, a);
+    time(keccakf_x1_avx512, b);
+    return time(keccakf_x1_avx512, b) < time(keccakf_scalar, a);
+}
 void keccakf(uint64_t s[25]) {
-    if (have_avx512()) keccakf_x1_avx512(s);
+    static const bool avx = pick_avx512_x1();
+    if (avx) keccakf_x1_avx512(s);
     else keccakf_scalar(s);
 }
 static inline void perm_bytes(uint8_t st[200]) {

@@ -68,6 +68,11 @@ GenSet::~GenSet() {
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
 }
+FbTables::~FbTables() {
+    if (G || H) (void)hipSetDevice(device);
+    if (G) (void)hipFree(G);
+    if (H) (void)hipFree(H);
+}
 CombTables::~CombTables() {
     if (tabG || tabH) (void)hipSetDevice(device);
     if (tabG) (void)hipFree(tabG);
@@ -285,6 +290,31 @@ std::shared_ptr<CombTables> DeviceContext::comb(const std::shared_ptr<const GenS
     BPG_HIP(hipDeviceSynchronize());
     combs[key] = t;
     comb_ms += now_ms() - t0;
+    return t;
+}
+
+std::shared_ptr<FbTables> DeviceContext::fb(const std::shared_ptr<const GenSet> &gs, uint32_t N) {
+    if (!gs || gs->world != 1 || N < 2 || N > (1u << 20) || gs->N < N) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = fbs.find(N);
+    if (it != fbs.end()) return it->second;
+    const size_t bytes = (size_t)dev::FB_W * 2 * N * sizeof(dev::NielsD);   // per vector
+    BPG_HIP(hipSetDevice(device));
+    size_t free_b = 0, total_b = 0;
+    BPG_HIP(hipMemGetInfo(&free_b, &total_b));
+    if (2 * bytes + std::max<size_t>((size_t)8 << 30, total_b / 32) > free_b) return nullptr;
+    std::shared_ptr<FbTables> t(new FbTables());
+    t->device = device;
+    t->N = N;
+    t->bytes = 2 * bytes;
+    if (hipMalloc(&t->G, bytes) != hipSuccess || hipMalloc(&t->H, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    launch_fb_build(gs->G, N, t->G, 0);
+    launch_fb_build(gs->H, N, t->H, 0);
+    BPG_HIP(hipDeviceSynchronize());
+    fbs[N] = t;
     return t;
 }
 
@@ -608,6 +638,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
         // circuit-independent, outside any timed region
         DeviceContext &ctx = DeviceContext::get(device);
         std::shared_ptr<const GenSet> gs = ctx.gens(P->N, rank, world);
+        if (strat.fixed_base()) ctx.fb(gs, P->N);
         if (strat.tables()) ctx.comb(gs, P->Nl);
     }
     return P;
@@ -746,6 +777,7 @@ ProducerStage::~ProducerStage() {
         if (ev[b]) (void)hipEventDestroy(ev[b]);
         if (drawn[b]) (void)hipEventDestroy(drawn[b]);
     }
+    if (one) (void)hipHostFree(one);
     if (st) (void)hipStreamDestroy(st);
 }
 
@@ -788,13 +820,25 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
             for (int k = count; k < 8; k++) wp[k] = tmp[k];
             draw(wp);
         }
-    } else if (count == 1 && out[0]->stage) {
-        // one proof: draws straight into its pinned buffer, copied up 2 MB at
-        // a time while the next ones are drawn (nothing waits on a copy); the
-        // s_L half ends a chunk, so its copy is the progress point
+    } else if (count == 1) {
+        // one proof: draws straight into a pinned buffer of all of them
+        // (the caller's, else this thread's), copied up 2 MB at a time while
+        // the next ones are drawn (nothing waits on a copy); the s_L half
+        // ends a chunk, so its copy is the progress point
         ProducerStage &ps = producer_stage(cs.device);
         const uint64_t BIG = 32768;
         uint8_t *h = out[0]->stage;
+        if (!h) {
+            if (ps.one_cap < 64 * nd) {
+                if (ps.one) BPG_HIP(hipHostFree(ps.one));
+                ps.one = nullptr;
+                BPG_HIP(hipHostMalloc((void **)&ps.one, 64 * nd, hipHostMallocDefault));
+                ps.one_cap = 64 * nd;
+            }
+            h = ps.one;
+            // the previous proof's copies out of this buffer are complete
+            BPG_HIP(hipEventSynchronize(ps.drawn[1]));
+        }
         for (int v = 0; v < 2; v++) {
             const uint64_t a = v ? nd / 2 : 0, b = v ? nd : nd / 2;
             for (uint64_t i0 = a; i0 < b; i0 += BIG) {
@@ -934,12 +978,16 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     B.sL.grow((size_t)nl * sizeof(ScD) + 64);
     B.sR.grow((size_t)nl * sizeof(ScD) + 64);
     CommitPre pre;
-    const int64_t gneg = gs->N;
+    std::shared_ptr<FbTables> fbt = (cs.world == 1 && cs.strat.fixed_base()) ? ctx.fb(gs, cs.N) : nullptr;
+    const void *G0 = fbt ? (const void *)fbt->G : (const void *)gs->G;
+    const void *H0 = fbt ? (const void *)fbt->H : (const void *)gs->H;
+    const int64_t gneg = fbt ? (int64_t)fbt->N : (int64_t)gs->N;
+    const uint64_t gws = fbt ? 2 * (uint64_t)fbt->N : 0;
     PtD *rows = ws.rows_host, *rows_dev = ws.rows_view;
     if (nl) {
-        const MsmSeg sa[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), gs->G, nl, 0, gneg},
-                              {as<ScD>(const_cast<DBuf &>(cs.aR)), gs->H, nl, 0, gneg},
-                              {as<ScD>(const_cast<DBuf &>(cs.aO)), gs->G, nl, 1, gneg}};
+        const MsmSeg sa[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg, gws},
+                              {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg, gws},
+                              {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws}};
         int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
         pre.A = ws.msm->enqueue(sa, 3, 2, rows + CommitPre::ROWS_A, MSM_NIELS, rows_dev + CommitPre::ROWS_A);
         ws.prof_end(ph);
@@ -949,7 +997,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         BPG_HIP(hipStreamWaitEvent(ws.st, drawn, 0));
         ScD *s = as<ScD>(v ? B.sR : B.sL);
         launch_wide_reduce(as<uint8_t>(B.wide) + (size_t)v * 64 * n, nl, cs.world, cs.rank, s, ws.st);
-        const MsmSeg seg = {s, v ? gs->H : gs->G, nl, 0, gneg};
+        const MsmSeg seg = {s, v ? H0 : G0, nl, 0, gneg, gws};
         const size_t off = v ? CommitPre::ROWS_S1 : CommitPre::ROWS_S0;
         int ph = ws.prof_begin("msm_commit", 1.0 * nl * (64 + 32));
         pre.S[v] = ws.msm->enqueue(&seg, 1, 1, rows + off, MSM_NIELS, rows_dev + off);
@@ -1048,8 +1096,14 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     // zero copy: the MSM row kernels and the c_L / c_R reductions write into
     // the pinned buffers through their device views (no copy launch per job)
     PtD *rowsA_dev = ws.rows_view, *rowsLR_dev = ws.rows_view + ROWS_HALF;
-    const void *G0 = gs->G, *H0 = gs->H;   // level-0 generators (affine Niels)
-    const int64_t gneg = gs->N;             // their negations follow each vector
+    // level-0 generators (affine Niels) for the MSM jobs: the fixed-base
+    // tables when this set has them (window 0 = the generators, negations
+    // at + N, window w at + w 2N), else the set itself (negations at + N)
+    std::shared_ptr<FbTables> fbt = (!sharded && cs.strat.fixed_base()) ? ctx.fb(gs, N) : nullptr;
+    const void *G0 = fbt ? (const void *)fbt->G : (const void *)gs->G;
+    const void *H0 = fbt ? (const void *)fbt->H : (const void *)gs->H;
+    const int64_t gneg = fbt ? (int64_t)fbt->N : (int64_t)gs->N;
+    const uint64_t gws = fbt ? 2 * (uint64_t)fbt->N : 0;   // MsmSeg::wstride of their segments
     // one commitment job per proof: a P-proof commitment job would be the
     // largest of the proof and size every workspace's MSM scratch (~7 GB at
     // P = 2 and 2^20), leaving HBM for fewer consumers
@@ -1074,11 +1128,11 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             }
             launch_wide_reduce(wd, nl, world, rank, as<ScD>(B.sL), st);
             launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(B.sR), st);
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg};
-            seg[nseg++] = {as<ScD>(B.sL), G0, nl, 2, gneg};
-            seg[nseg++] = {as<ScD>(B.sR), H0, nl, 2, gneg};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg, gws};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg, gws};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws};
+            seg[nseg++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
+            seg[nseg++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};
         }
         for (int p = 0; p < P && nseg; p++) {
             int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
@@ -1361,6 +1415,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                 for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
             }
         }
+        if (mfmt == MSM_NIELS)   // level-0 generator segments gather from the fixed-base tables
+            for (int i = 0; i < nseg; i++) seg[i].wstride = gws;
         int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt, rowsLR_dev);
         ws.prof_end(ph);

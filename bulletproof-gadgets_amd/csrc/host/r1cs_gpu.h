@@ -48,11 +48,25 @@ struct CombTables {
     size_t bytes = 0;
     ~CombTables();
 };
+// Fixed-base tables of the first N generators of a full set (world 1):
+// FB_W windows of 2^(FB_C w) G_i and H_i with their negations, affine Niels
+// (dev::launch_fb_build): the commitment and IPP round-0/1 MSM jobs then put
+// all 13 windows of a point into one bucket row, 13 additions per point
+// instead of 16 (~7 GB at N = 2^20).
+struct FbTables {
+    int device = 0;
+    uint32_t N = 0;
+    dev::NielsD *G = nullptr, *H = nullptr;   // FB_W x 2N points each
+    size_t bytes = 0;
+    ~FbTables();
+};
 // IPP fold strategy, per context (bpg_ctx_set_fold_tables / _pairs / _ipp_tail):
 // -1 default (tables on, round triples, tail at 4096 lanes), 0 off, 1 on.
 // Proof bytes are identical under every strategy.
 struct Strategy {
     int fold_tables = -1, fold_pairs = -1;
+    int msm_tables = -1;   // fixed-base generator tables (bpg_ctx_set_msm_tables): -1 / 1 on, 0 off
+    bool fixed_base() const { return msm_tables != 0; }
     int ipp_tail = -1;   // IPP tail threshold in lanes (-1: 4096)
     uint32_t tail() const;
     bool tables() const;
@@ -70,6 +84,7 @@ struct DeviceContext {
     std::shared_ptr<const GenSet> full;   // the largest full set derived so far
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::shared_ptr<const GenSet>> slices;   // (N, rank, world)
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::shared_ptr<CombTables>> combs;      // (N, rank, world)
+    std::map<uint32_t, std::shared_ptr<FbTables>> fbs;                                          // N
     PtD *tabB = nullptr, *tabBb = nullptr;
     PtD *Bb = nullptr;                  // B_blinding as a device point
     double gens_ms = 0, comb_ms = 0;    // time spent deriving / building (cold-setup breakdown)
@@ -84,6 +99,10 @@ struct DeviceContext {
     // cached per (N, slice); null when N < 8 or when they would not fit in
     // free HBM (tables not in use are evicted first).
     std::shared_ptr<CombTables> comb(const std::shared_ptr<const GenSet> &gs, uint32_t N);
+    // Fixed-base tables over the first N points of a full set, built on
+    // first use; null when sharded, when N > 2^20 (an entry's 25-bit index
+    // must reach window 12) or when they would not fit in free HBM.
+    std::shared_ptr<FbTables> fb(const std::shared_ptr<const GenSet> &gs, uint32_t N);
 };
 // On-disk cache of the derived generators: directory from
 // bpg_gens_cache_dir() or env BPG_GENS_CACHE; empty = off.
@@ -150,11 +169,16 @@ struct RngBlock {
 };
 // Per-thread staging of RNG output into device buffers.
 struct ProducerStage {
-    static const uint32_t CHUNK = 2048;   // draws per staged chunk
+    // draws per staged chunk: 8 x 16384 x 64 B = 8 MB per staging buffer, so
+    // a group of eight 2^20 proofs takes 91 chunks (728 per proof before:
+    // the copy calls and event polls were ~10% of a producer's time)
+    static const uint32_t CHUNK = 16384;
     hipStream_t st = nullptr;                 // this producer thread's copy stream
     uint8_t *host[2] = {nullptr, nullptr};   // pinned, 8 x CHUNK x 64 B each
     hipEvent_t ev[2] = {nullptr, nullptr};
     hipEvent_t drawn[2] = {nullptr, nullptr};   // s_L / s_R copies complete (rng_draw_group's progress)
+    uint8_t *one = nullptr;                  // pinned, all draws of a one-proof group (grown)
+    size_t one_cap = 0;
     ~ProducerStage();
 };
 ProducerStage &producer_stage(int device);

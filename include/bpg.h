@@ -187,6 +187,14 @@ void bpg_ctx_destroy(bpg_ctx *ctx);
  *     sharded prover uses the same grouping. */
 int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode);
 int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
+/* Fixed-base generator tables for the MSMs over the generators (the
+ * commitments A_I1, A_O1, S1 and IPP rounds 0-1) of `ctx`'s calls: 13 windows
+ * of 20 bits with 2^(20w) G_i, 2^(20w) H_i precomputed (and negated) for
+ * the first N generators, so all windows of a point share one bucket row:
+ * 13 additions per point instead of 16. 1 on, 0 off, -1 (default) on where
+ * they fit (N <= 2^20, one rank, ~7 GB of HBM at N = 2^20). Proof bytes are
+ * identical either way. */
+int bpg_ctx_set_msm_tables(bpg_ctx *ctx, int mode);
 /* IPP tail threshold of `ctx`'s calls: once a materialised generator level
  * has at most `lanes` points, the remaining rounds weight its points instead
  * of folding them (-1, the default: env BPG_IPP_TAIL, else 4096). Proof bytes
@@ -198,7 +206,8 @@ int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes);
 /* Cold-setup breakdown of the device `ctx` is on: out[0] ms spent deriving
  * (or loading) generators, out[1] ms building comb tables, out[2] 1 if the
  * generators came from the on-disk cache, out[3] ms of out[1] spent
- * allocating the tables' memory, out[4] bytes of comb tables resident. */
+ * allocating the tables' memory, out[4] bytes of comb tables resident,
+ * out[5] bytes of fixed-base MSM tables resident (n <= 6). */
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n);
 /* Release the device's cached comb tables and sharded generator slices that
  * no proof in flight holds, and the batch worker pool's (and the caller's)

@@ -14,7 +14,7 @@ ROOTD=$(pwd)
 db=$(find /tmp/${R}_prof -name '*.db' -print -quit)
 python3 scripts/prof_summary.py "$db" gpurun_out/${R}_profdefault_kernels.md > /dev/null || exit $?
 python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline_default.md 0.92 > /dev/null || exit $?
-R=${R} ARGS="--steps 1 --warmup 1 --threads 8 --batch 32 --no-cpu-baseline" bash scripts/r02_pmc.sh || exit $?
+R=${R} ARGS="--steps 1 --warmup 1 --threads 8 --batch 32 --no-cpu-baseline" bash scripts/pmc_passes.sh || exit $?
 python3 scripts/pmc_table.py gpurun_out/${R} gpurun_out/${R}_pmc.json > gpurun_out/${R}_pmc_table.md || exit $?
 timeout -k 10 300 python bench.py --mode verify --steps 3 --warmup 1 > gpurun_out/${R}_verify.json 2> gpurun_out/${R}_verify.err || exit $?
 timeout -k 10 300 python bench.py --mode verify-sharded --steps 20 --warmup 3 > gpurun_out/${R}_verify_sharded.json 2> gpurun_out/${R}_verify_sharded.err || exit $?

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel roofline table from the reduced PMC passes of scripts/r02_pmc.sh
+"""Per-kernel roofline table from the reduced PMC passes of scripts/pmc_passes.sh
 (pmc0 FETCH_SIZE, pmc1 WRITE_SIZE, pmc2 SQ issue/wait counters, pmc3
 GRBM_GUI_ACTIVE), every pass a kernel-trace + one counter group. Counter
 collection serialises the dispatches, so the durations are per-kernel

@@ -153,6 +153,28 @@ def test_fold_strategy_bit_exact(bpg, resources, name, tables, pairs, tail):
     assert proof == o_proof
 
 
+@pytest.mark.parametrize("msm_tables,tail", [(0, -1), (1, -1), (1, 8), (0, 8)])
+@pytest.mark.parametrize("name", ["bounds_check", "example", "or5"])
+def test_msm_tables_bit_exact(bpg, resources, name, msm_tables, tail):
+    """Fixed-base generator tables (bpg_ctx_set_msm_tables: 13 windows of
+    2^(20w) G_i / H_i, one bucket row per MSM) for the commitment and IPP
+    round-0/1 jobs, or the ordinary 16-window jobs: the oracle's bytes
+    either way, with the default and a small IPP tail threshold."""
+    fx = read_fixture(os.path.join(resources, name))
+    seed = 700 + len(name)
+    st = S.synthesize_prover(fx["inst"], fx["wtns"], fx["gadgets"], seed)
+    flat = st.cs.to_flat()
+    ent = S.entropy_for(st)
+    o_proof, o_V = O.r1cs_prove(name.encode(), flat, ent)
+    c = bpg.Context(0)
+    c.set_strategy(ipp_tail=tail, msm_tables=msm_tables)
+    proof, V = c.r1cs_prove(name.encode(), flat.view(), ent)
+    assert V == o_V
+    assert proof == o_proof
+    if msm_tables:
+        assert c.setup_stats()["msm_table_bytes"] > 0
+
+
 @pytest.mark.parametrize("name", ["bounds_check", "less_than", "example"])
 def test_fixture_rejects(bpg, resources, name):
     fx = read_fixture(os.path.join(resources, name))

@@ -49,6 +49,6 @@ def test_prove_statements_matches_c_prove(bpg):
     st = bpg.last_statements_stats()
     assert st["workers"] == 6 and st["consumers"] == 3
     assert st["est_gb_per_statement"] > 0 and st["hbm_limit"] >= st["consumers"] + 1
-    assert st["limit"] <= 6 + 8 + 2 * 3
+    assert st["limit"] <= 4 * 6 + 8 + 2 * 3
     assert st["bound_stage"] in ("cpu workers (synthesis + prepare + rng)", "device consumers")
     assert st["synth_ms"] > 0 and st["prove_ms"] > 0 and st["rng_ms"] > 0
