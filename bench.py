@@ -510,7 +510,7 @@ def main():
                    "parallelism": "independent proofs per GPU (%d ranks)" % world,
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
                    "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables],
-                   "msm_fixed_base_tables": {-1: "default (on where they fit)", 0: "off", 1: "on"}[a.msm_tables]},
+                   "msm_fixed_base_tables": {-1: "default (on from 2^18 generators, where HBM holds them)", 0: "off", 1: "on"}[a.msm_tables]},
         "host_cores_busy": round(host_busy, 2),
         # the producer/consumer pipeline of the timed batch (bpg_last_batch_stats):
         # consumer time starved of ready proofs while producers were drawing

@@ -397,10 +397,10 @@ __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist,
 // rank keys within their digit, the iteration is reordered by digit in LDS,
 // then written out so that lanes with consecutive LDS slots of one digit
 // write consecutive addresses.
-// STABLE = false (every pass but the last of an LSD sort: the next pass
-// reorders by a higher digit anyway, and equal keys are interchangeable in
-// the MSM): keys are ranked within their digit by LDS atomics instead of the
-// wave ballots.
+// STABLE = false (the first pass of an LSD sort: it has no earlier order to
+// keep, and equal keys are interchangeable in the MSM): keys are ranked
+// within their digit by LDS atomics instead of the wave ballots. Every later
+// pass must keep the order of the passes before it.
 template <int RS_BITS, bool STABLE>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                          int shift, const uint32_t *__restrict__ tiles, uint32_t nb,
@@ -975,22 +975,22 @@ static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2,
     const int bits = (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
-    const int passes = (key_bits + bits - 1) / bits;
     for (int shift = 0; shift < key_bits; shift += bits) {
-        // only the last of several passes must keep the order of equal digits
-        const bool last = passes > 1 && shift + bits >= key_bits;
+        // every pass after the first keeps the order of equal digits (the
+        // three-pass sorts of 20-bit fixed-base keys need the middle one too)
+        const bool stable = shift > 0;
         if (bits == 8)
             hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         else
             hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         hipLaunchKernelGGL(k_rs_colscan, dim3(bins), dim3(256), 0, st, hist, nt, total);
-        if (bits == 8 && last)
+        if (bits == 8 && stable)
             hipLaunchKernelGGL((k_rs_scatter<8, true>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
                                total, k2, v2);
         else if (bits == 8)
             hipLaunchKernelGGL((k_rs_scatter<8, false>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
                                total, k2, v2);
-        else if (last)
+        else if (stable)
             hipLaunchKernelGGL((k_rs_scatter<7, true>), dim3(nt), dim3(RS_BLOCK), 0, st, k, v, shift, tiles, nt, hist,
                                total, k2, v2);
         else

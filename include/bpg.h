@@ -191,13 +191,14 @@ int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
  * commitments A_I1, A_O1, S1 and IPP rounds 0-1) of `ctx`'s calls: 13 windows
  * of 20 bits with 2^(20w) G_i, 2^(20w) H_i precomputed (and negated) for
  * the first N generators, so all windows of a point share one bucket row:
- * 13 additions per point instead of 16. 1 on, 0 off, -1 (default) on where
- * they fit (N <= 2^20, one rank, ~7 GB of HBM at N = 2^20). Proof bytes are
- * identical either way. */
+ * 13 additions per point instead of 16-17. 1 on (any N), 0 off, -1 (default)
+ * on for 2^18 <= N <= 2^20 (below, their 2^19-bucket rows cost more than the
+ * windows they save), one rank, when HBM holds them (~7 GB at N = 2^20).
+ * Proof bytes are identical either way. */
 int bpg_ctx_set_msm_tables(bpg_ctx *ctx, int mode);
 /* IPP tail threshold of `ctx`'s calls: once a materialised generator level
  * has at most `lanes` points, the remaining rounds weight its points instead
- * of folding them (-1, the default: env BPG_IPP_TAIL, else 4096). Proof bytes
+ * of folding them (-1, the default: 4096). Proof bytes
  * are identical for every threshold; small values exercise the fold passes on
  * small circuits. The sharded prover must end its local rounds in the tail
  * and uses max(lanes, 8). */

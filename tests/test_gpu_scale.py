@@ -68,13 +68,15 @@ def test_full_size_verify_and_strategies(bpg, W, cfg):
     syn = bpg.Synth(inst, wit, gad)
     ent = bytes([cfg]) * 32
     proofs = []
-    # (comb tables, round grouping): the production default (table pass +
-    # Straus triple folds), table pass + Straus pair folds, Straus triple
-    # folds only, Straus pair folds only, one variable-base fold per round;
-    # each through its own context (strategies are per context)
-    for tables, pairs in ((-1, -1), (1, 1), (0, 2), (0, 1), (0, 0)):
+    # (comb tables, round grouping, fixed-base MSM tables): the production
+    # default (table pass + Straus triple folds, fixed-base tables from 2^18
+    # generators), table pass + Straus pair folds, Straus triple folds only,
+    # Straus pair folds only, one variable-base fold per round, with the
+    # fixed-base tables forced on or off; each through its own context
+    # (strategies are per context)
+    for tables, pairs, msm in ((-1, -1, -1), (1, 1, 0), (0, 2, 1), (0, 1, -1), (0, 0, 0), (-1, -1, 1)):
         c = bpg.Context(0)
-        c.set_strategy(tables, pairs)
+        c.set_strategy(tables, pairs, msm_tables=msm)
         p, V = c.r1cs_prove(b"scale", syn.view, ent)
         proofs.append(p)
     assert all(p == proofs[0] for p in proofs)
