@@ -840,10 +840,11 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
         ge_add(acc, acc, run);
     }
     // run and acc wait out the scan in this thread's first two segT slots
-    // (their T_s are consumed); with one segment acc = run, with none both
-    // are the identity
+    // (their T_s are consumed); with one segment (K = 1, or the row's last
+    // thread) acc = run, with none both are the identity. Slot s0 + 1 is
+    // this thread's only when K >= 2.
     const uint32_t s0 = t * K;
-    const bool has = s0 < nseg, two = has && s0 + 1 < nseg;
+    const bool has = s0 < nseg, two = has && K >= 2 && s0 + 1 < nseg;
     if (has) ge_store(T + s0, run);
     if (two) ge_store(T + s0 + 1, acc);
     // inclusive suffix scan of run over threads
