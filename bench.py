@@ -55,6 +55,9 @@ def parse():
                          "Default: producers + 8 (verify mode 24)")
     ap.add_argument("--producers", type=int, default=0,
                     help="TranscriptRng producer threads per GPU (default: one per CPU of the rank's share, at most 8)")
+    ap.add_argument("--max-inflight", type=int, default=0,
+                    help="proofs in flight per GPU (bpg_ctx_set_pipeline max_inflight; 0: 24 at 2^20, and what HBM "
+                         "admits)")
     ap.add_argument("--cpus", type=int, default=0,
                     help="pin this rank to its first N CPUs (emulates the per-rank CPU share of a multi-GPU node)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -62,7 +65,7 @@ def parse():
                     help="IPP comb tables: 1 on, 0 off (the path a device without ~208 GB free takes), -1 default")
     ap.add_argument("--msm-tables", type=int, default=-1, choices=(-1, 0, 1),
                     help="fixed-base generator tables for the MSMs over the generators (13 windows of 20 bits, "
-                         "~7 GB at 2^20): 1 on, 0 off, -1 default (on where they fit)")
+                         "~7 GB at 2^20): 1 on, 0 or -1 (the default) off")
     ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification); latency: one proof at a time, sharded over all "
@@ -365,7 +368,7 @@ def main():
     ctx = bpg.Context(dev)
     if a.fold_tables >= 0 or a.msm_tables >= 0:
         ctx.set_strategy(fold_tables=a.fold_tables, msm_tables=a.msm_tables)
-    ctx.set_pipeline(producers=min(producers, 8))
+    ctx.set_pipeline(producers=min(producers, 8), max_inflight=a.max_inflight)
     if a.mode == "latency":
         return bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W)
     # cold setup, outside the timed region: BulletproofGens::new (prove.rs:78,
@@ -510,7 +513,7 @@ def main():
                    "parallelism": "independent proofs per GPU (%d ranks)" % world,
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
                    "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables],
-                   "msm_fixed_base_tables": {-1: "default (on from 2^18 generators, where HBM holds them)", 0: "off", 1: "on"}[a.msm_tables]},
+                   "msm_fixed_base_tables": {-1: "default (off)", 0: "off", 1: "on"}[a.msm_tables]},
         "host_cores_busy": round(host_busy, 2),
         # the producer/consumer pipeline of the timed batch (bpg_last_batch_stats):
         # consumer time starved of ready proofs while producers were drawing

@@ -1954,37 +1954,11 @@ DEVI void foldn_get(gec &c, const uint32_t *tb) {
 #pragma unroll
     for (int k = 0; k < 40; k++) w[k] = tb[k * 64];
 }
-#ifndef FOLD3_LAZY
-#define FOLD3_LAZY 0
-#endif
 // waves per SIMD the triple fold is compiled for (332 VGPRs; at 2 waves
-// it spilled and measured slower, profiles/r03c_ab_commitjob_fold3_smallmsm.txt)
-static constexpr int FOLD3_WAVES = FOLD3_LAZY ? 2 : 1;
-// one coordinate of a table entry (word-major, lane stride 64)
-DEVI void foldn_get_fe(fe &x, const uint32_t *tb) {
-#pragma unroll
-    for (int k = 0; k < 10; k++) x.v[k] = tb[k * 64];
-}
-// acc + (SUB: -) the cached point of table entry `e`, each coordinate loaded
-// right before its product: 10 live registers for the operand, not 40
-template <bool SUB>
-DEVI void ge_addsub_tab(ge &r, const ge &p, const uint32_t *e) {
-    fe a, b, c, d, q;
-    foldn_get_fe(q, e + (SUB ? 0 : 10) * 64);   // Y-X (Y+X for -P)
-    fe_sub_nc(a, p.Y, p.X); fe_mul(a, a, q);
-    foldn_get_fe(q, e + (SUB ? 10 : 0) * 64);   // Y+X (Y-X for -P)
-    fe_add_nc(b, p.Y, p.X); fe_mul(b, b, q);
-    foldn_get_fe(q, e + 30 * 64);                // 2dT
-    fe_mul(c, p.T, q);
-    foldn_get_fe(q, e + 20 * 64);                // 2Z
-    fe_mul(d, p.Z, q);
-    fe ee, f, g, h;
-    fe_sub_nc(ee, b, a);
-    if (SUB) { fe_add_nc(f, d, c); fe_sub_nc(g, d, c); }
-    else { fe_sub_nc(f, d, c); fe_add_nc(g, d, c); }
-    fe_add_nc(h, b, a);
-    fe_mul(r.X, ee, f); fe_mul(r.Y, g, h); fe_mul(r.T, ee, h); fe_mul(r.Z, f, g);
-}
+// it spilled and measured slower, profiles/r03c_ab_commitjob_fold3_smallmsm.txt;
+// a 2-wave form loading each table operand coordinate by coordinate fit
+// without spills but measured 1.2% slower, profiles/r04l_ab.txt)
+static constexpr int FOLD3_WAVES = 1;
 // the lane's odd multiples P, 3P, .. of the seven points into the block's
 // word-major table
 template <class P>
@@ -2029,18 +2003,6 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
-#if FOLD3_LAZY
-    for (uint32_t k = 1; k < nops; k++) {
-        const uint32_t op = fold2_op(ops, k);
-        const uint32_t g = op & 255;
-        if (g) {
-            for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
-            ge_dbl_t<true>(acc, acc);
-        }
-        const uint32_t *e = foldn_entry(tb, op);
-        if (op >> 15) ge_addsub_tab<true>(acc, acc, e); else ge_addsub_tab<false>(acc, acc, e);
-    }
-#else
     // the next op's table entry is loaded before the doublings
     gec c;
     if (nops > 1) foldn_get(c, foldn_entry(tb, fold2_op(ops, 1)));
@@ -2059,7 +2021,6 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
         c = cn;
     }
-#endif
     const uint32_t tail = A.tail[sg];
     if (tail) {
         for (uint32_t j = 1; j < tail; j++) ge_dbl_t<false>(acc, acc);

@@ -638,7 +638,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
         // circuit-independent, outside any timed region
         DeviceContext &ctx = DeviceContext::get(device);
         std::shared_ptr<const GenSet> gs = ctx.gens(P->N, rank, world);
-        if (strat.fixed_base(P->N)) ctx.fb(gs, P->N);
+        if (strat.fixed_base()) ctx.fb(gs, P->N);
         if (strat.tables()) ctx.comb(gs, P->Nl);
     }
     return P;
@@ -978,7 +978,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     B.sL.grow((size_t)nl * sizeof(ScD) + 64);
     B.sR.grow((size_t)nl * sizeof(ScD) + 64);
     CommitPre pre;
-    std::shared_ptr<FbTables> fbt = (cs.world == 1 && cs.strat.fixed_base(cs.N)) ? ctx.fb(gs, cs.N) : nullptr;
+    std::shared_ptr<FbTables> fbt = (cs.world == 1 && cs.strat.fixed_base()) ? ctx.fb(gs, cs.N) : nullptr;
     const void *G0 = fbt ? (const void *)fbt->G : (const void *)gs->G;
     const void *H0 = fbt ? (const void *)fbt->H : (const void *)gs->H;
     const int64_t gneg = fbt ? (int64_t)fbt->N : (int64_t)gs->N;
@@ -1099,7 +1099,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     // level-0 generators (affine Niels) for the MSM jobs: the fixed-base
     // tables when this set has them (window 0 = the generators, negations
     // at + N, window w at + w 2N), else the set itself (negations at + N)
-    std::shared_ptr<FbTables> fbt = (!sharded && cs.strat.fixed_base(N)) ? ctx.fb(gs, N) : nullptr;
+    std::shared_ptr<FbTables> fbt = (!sharded && cs.strat.fixed_base()) ? ctx.fb(gs, N) : nullptr;
     const void *G0 = fbt ? (const void *)fbt->G : (const void *)gs->G;
     const void *H0 = fbt ? (const void *)fbt->H : (const void *)gs->H;
     const int64_t gneg = fbt ? (int64_t)fbt->N : (int64_t)gs->N;

@@ -65,12 +65,11 @@ struct FbTables {
 // Proof bytes are identical under every strategy.
 struct Strategy {
     int fold_tables = -1, fold_pairs = -1;
-    // fixed-base generator tables (bpg_ctx_set_msm_tables): 1 on, 0 off, -1
-    // on from FB_MIN_N generators (below it their 2^19-bucket rows cost more
-    // than the windows they save)
+    // fixed-base generator tables (bpg_ctx_set_msm_tables): 1 on; 0 and -1
+    // (the default) off: 5.7% slower with them in the bench, whose sixth
+    // consumer they crowd out of HBM (profiles/r04l_ab.txt)
     int msm_tables = -1;
-    static const uint32_t FB_MIN_N = 1u << 18;
-    bool fixed_base(uint32_t N) const { return msm_tables == 1 || (msm_tables == -1 && N >= FB_MIN_N); }
+    bool fixed_base() const { return msm_tables == 1; }
     int ipp_tail = -1;   // IPP tail threshold in lanes (-1: 4096)
     uint32_t tail() const;
     bool tables() const;

@@ -172,9 +172,8 @@ void bpg_ctx_destroy(bpg_ctx *ctx);
  * bpg_prepare; a prepared circuit keeps the strategy it was prepared with).
  * Proof bytes are identical under every strategy.
  *   fold_tables 1: comb tables of the generators fold IPP rounds 0-1 in one
- *     table pass; 0: per-round variable-base fold; -1 (default): on unless
- *     env BPG_FOLD_TABLES=0 (tables are skipped when they do not fit in free
- *     HBM). Footprint (default build, COMB_BITS 6): generators j in [N/4, N)
+ *     table pass; 0: per-round variable-base fold; -1 (default): on
+ *     (tables are skipped when they do not fit in free HBM). Footprint (default build, COMB_BITS 6): generators j in [N/4, N)
  *     of G and of H, COMB_WIN (43) windows x COMB_ENT (32) entries x 96 B
  *     each, i.e. 0.75 x 43 x 32 x 96 x 2 B = ~198 KB x N per device
  *     (208 GB at N = 2^20; a sharded rank holds the tables of its N/world
@@ -182,19 +181,19 @@ void bpg_ctx_destroy(bpg_ctx *ctx);
  *   fold_pairs 2: after the comb pass, rounds k, k+1, k+2 fold together
  *     (level k+3 from level k by a seven-scalar Straus pass; rounds k+1, k+2
  *     expand their bases into level-k points); 1: rounds fold in pairs
- *     (three-scalar Straus pass); 0: one fold per round; -1 (default): 2,
- *     or 1 with env BPG_FOLD_TRIPLES=0, or 0 with env BPG_FOLD_PAIRS=0. The
- *     sharded prover uses the same grouping. */
+ *     (three-scalar Straus pass); 0: one fold per round; -1 (default): 2.
+ *     The sharded prover uses the same grouping. */
 int bpg_ctx_set_fold_tables(bpg_ctx *ctx, int mode);
 int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
 /* Fixed-base generator tables for the MSMs over the generators (the
  * commitments A_I1, A_O1, S1 and IPP rounds 0-1) of `ctx`'s calls: 13 windows
  * of 20 bits with 2^(20w) G_i, 2^(20w) H_i precomputed (and negated) for
  * the first N generators, so all windows of a point share one bucket row:
- * 13 additions per point instead of 16-17. 1 on (any N), 0 off, -1 (default)
- * on for 2^18 <= N <= 2^20 (below, their 2^19-bucket rows cost more than the
- * windows they save), one rank, when HBM holds them (~7 GB at N = 2^20).
- * Proof bytes are identical either way. */
+ * 13 additions per point instead of 16-17. 1 on (one rank, N <= 2^20, when
+ * HBM holds them: ~7 GB at N = 2^20), 0 or -1 (the default) off: with them
+ * the bench proves 5.7% slower, as the tables crowd a consumer out of HBM and
+ * their gathers miss the cache the 256 MB generator set stays in. Proof bytes
+ * are identical either way. */
 int bpg_ctx_set_msm_tables(bpg_ctx *ctx, int mode);
 /* IPP tail threshold of `ctx`'s calls: once a materialised generator level
  * has at most `lanes` points, the remaining rounds weight its points instead

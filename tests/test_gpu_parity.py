@@ -158,10 +158,9 @@ def test_fold_strategy_bit_exact(bpg, resources, name, tables, pairs, tail):
 def test_msm_tables_bit_exact(bpg, resources, name, msm_tables, tail):
     """Fixed-base generator tables (bpg_ctx_set_msm_tables: 13 windows of
     2^(20w) G_i / H_i, one bucket row per MSM, keys sorted in three radix
-    passes) for the commitment and IPP round-0/1 jobs, forced on at these
-    small sizes (the default takes them from 2^18 generators), or the
-    ordinary windowed jobs: the oracle's bytes either way, with the default
-    and a small IPP tail threshold."""
+    passes) for the commitment and IPP round-0/1 jobs (on), or the ordinary
+    windowed jobs (off, and the default): the oracle's bytes either way, with
+    the default and a small IPP tail threshold."""
     fx = read_fixture(os.path.join(resources, name))
     seed = 700 + len(name)
     st = S.synthesize_prover(fx["inst"], fx["wtns"], fx["gadgets"], seed)

@@ -69,8 +69,8 @@ def test_full_size_verify_and_strategies(bpg, W, cfg):
     ent = bytes([cfg]) * 32
     proofs = []
     # (comb tables, round grouping, fixed-base MSM tables): the production
-    # default (table pass + Straus triple folds, fixed-base tables from 2^18
-    # generators), table pass + Straus pair folds, Straus triple folds only,
+    # default (table pass + Straus triple folds, windowed generator MSMs),
+    # table pass + Straus pair folds, Straus triple folds only,
     # Straus pair folds only, one variable-base fold per round, with the
     # fixed-base tables forced on or off; each through its own context
     # (strategies are per context)
