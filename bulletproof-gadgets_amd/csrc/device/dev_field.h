@@ -435,6 +435,12 @@ DEVI void gec_neg(gec &r, const gec &c) { r.YpX = c.YmX; r.YmX = c.YpX; r.Z2 = c
 DEVI void gec_cneg(gec &c, bool neg) {
     if (neg) { fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; fe_neg(c.T2d, c.T2d); }
 }
+// Operand roles in the four output products: fe_mul(h, f, g) doubles the odd
+// limbs of f and multiplies g by 19, so the formulas pair the outputs'
+// factors as two sets, one always first and one always second (X = e f,
+// Y = g h, T = e h, Z = g f): each set's premultiplied limbs are computed
+// once and shared by its two products (14 fewer instructions per addition),
+// with the g side within 3T as fe_mul requires.
 // add-2008-hwcd-3 (a = -1) with a cached right operand: 8M; with_t = false
 // skips T (7M) for an addition followed by a doubling (T is not an input of
 // doubling), as ge_dbl_t does.
@@ -449,7 +455,7 @@ DEVI void ge_add_c_t(ge &r, const ge &p, const gec &q) {
     fe_sub_nc(f, d, c);                                 // 3T
     fe_add_nc(g, d, c);                                 // 2T
     fe_add_nc(h, b, a);                                 // 2T
-    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); if (with_t) fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); if (with_t) fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
 }
 template <bool with_t>
 DEVI void ge_sub_c_t(ge &r, const ge &p, const gec &q) {
@@ -479,7 +485,7 @@ DEVI void ge_madd(ge &r, const ge &p, const gen &q) {
     fe_sub_nc(f, d, c);
     fe_add_nc(g, d, c);
     fe_add_nc(h, b, a);
-    fe_mul(r.X, f, e); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+    fe_mul(r.X, f, e); fe_mul(r.Y, h, g); fe_mul(r.T, h, e); fe_mul(r.Z, f, g);
 }
 DEVI void gen_cneg(gen &c, bool neg) {
     if (neg) { fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; fe_neg(c.T2d, c.T2d); }
@@ -521,7 +527,7 @@ DEVI void ge_add(ge &r, const ge &p, const ge &q) {
     fe_sub_nc(f, d, c);
     fe_add_nc(g, d, c);
     fe_add_nc(h, b, a);
-    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
 }
 DEVI void ge_neg(ge &r, const ge &p) { fe_neg(r.X, p.X); r.Y = p.Y; r.Z = p.Z; fe_neg(r.T, p.T); }
 DEVI void ge_sub(ge &r, const ge &p, const ge &q) { ge n; ge_neg(n, q); ge_add(r, p, n); }
@@ -537,7 +543,7 @@ DEVI void ge_dbl_t(ge &r, const ge &p) {
     fe_sub_nc(ymx, yy, xx);                             // 3T
     fe_sub4_nc(ex, xpy2, ypx);                          // 5T
     fe_sub4_nc(tc, zz2, ymx); fe_carry(tc, tc);         // 6T -> T
-    fe_mul(r.X, ex, tc); fe_mul(r.Y, ypx, ymx); fe_mul(r.Z, ymx, tc);
+    fe_mul(r.X, ex, tc); fe_mul(r.Y, ymx, ypx); fe_mul(r.Z, ymx, tc);
     if (with_t) fe_mul(r.T, ex, ypx);
 }
 DEVI void ge_dbl(ge &r, const ge &p) { ge_dbl_t<true>(r, p); }

@@ -804,7 +804,7 @@ DEVI void ge_add_mem(ge &r, const ge &p, const ge *q) {
     fe_add_nc(u, u, u); fe_mul(d, p.Z, u);
     fe e, f, g, h;
     fe_sub_nc(e, b, a); fe_sub_nc(f, d, c); fe_add_nc(g, d, c); fe_add_nc(h, b, a);
-    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, f, g);
+    fe_mul(r.X, e, f); fe_mul(r.Y, g, h); fe_mul(r.T, e, h); fe_mul(r.Z, g, f);
 }
 // Level 2, one block per row; thread t owns segments [tK, tK + K):
 //   sum_s s T_s = sum_t (acc_t - run_t) + K * sum_t t run_t,
