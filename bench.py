@@ -55,6 +55,8 @@ def parse():
                          "Default: producers + 8 (verify mode 24)")
     ap.add_argument("--producers", type=int, default=0,
                     help="TranscriptRng producer threads per GPU (default: one per CPU of the rank's share, at most 8)")
+    ap.add_argument("--consumers", type=int, default=0,
+                    help="statements mode: device threads (bpg_set_statements_consumers; 0: threads / 2)")
     ap.add_argument("--max-inflight", type=int, default=0,
                     help="proofs in flight per GPU (bpg_ctx_set_pipeline max_inflight; 0: 24 at 2^20, and what HBM "
                          "admits)")
@@ -775,6 +777,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         api = "c_prove on %d threads" % threads
         stages = None
     else:   # bpg_prove_statements: lockstep RNG over distinct statements, device consumers
+        bpg.set_statements_consumers(a.consumers)
         bpg.prove_statements("bench", texts[:batch * a.warmup], threads)
         barrier()
         t0 = time.perf_counter()
@@ -784,7 +787,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         stages = bpg.last_statements_stats()
         if any(o is None for o in outs):
             raise SystemExit("bench: a statement failed: %s" % bpg.last_error())
-        api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(16, max(1, threads // 2)))
+        api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(16, max(1, a.consumers or threads // 2)))
     if dist is not None:
         dt = D.max_over_ranks(dt)
     last = texts[-1]

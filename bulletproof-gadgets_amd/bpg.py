@@ -33,6 +33,7 @@ EXPORTS = [
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
     "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim", "bpg_prove_statements",
     "bpg_ctx_set_pipeline", "bpg_last_batch_stats", "bpg_last_statements_stats", "bpg_ctx_set_msm_tables",
+    "bpg_set_statements_consumers",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -98,6 +99,7 @@ def lib():
         L.bpg_ctx_set_msm_tables.argtypes = [vp, ctypes.c_int]
         L.bpg_last_batch_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_last_statements_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.bpg_set_statements_consumers.argtypes = [u32]
         L.bpg_r1cs_prove_sharded.argtypes = [vp, vp, sz, vp, vp, u32, u32, ALLGATHER_FN, vp, vp, sz,
                                              ctypes.POINTER(sz), vp]
         L.bpg_prepare.restype = vp
@@ -178,6 +180,13 @@ def prove(name, instance, witness, gadgets):
     finally:
         lib().free_proof(a)
     return proof, coms
+
+
+def set_statements_consumers(consumers):
+    """bpg_set_statements_consumers: device threads of later
+    prove_statements calls (0: threads / 2)."""
+    if lib().bpg_set_statements_consumers(consumers) != 0:
+        raise BpgError("statements consumers out of range")
 
 
 def prove_statements(name, statements, threads, seeds=None):
@@ -599,4 +608,7 @@ def last_statements_stats():
         int(d["bound_stage"]), "?")
     for k in ("workers", "consumers", "limit", "hbm_limit"):
         d[k] = int(d[k])
+    wall = max(d["wall_ms"], 1e-9)
+    d["worker_busy_frac"] = round(1 - d["worker_idle_ms"] / (wall * max(d["workers"], 1)), 3)
+    d["consumer_busy_frac"] = round(1 - d["consumer_idle_ms"] / (wall * max(d["consumers"], 1)), 3)
     return d

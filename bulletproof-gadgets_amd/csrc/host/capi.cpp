@@ -671,6 +671,7 @@ static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector
     return a;
 }
 namespace {
+std::atomic<uint32_t> g_stmt_consumers(0);   // bpg_set_statements_consumers (0: threads / 2)
 std::mutex g_ss_mu;
 double g_ss[13] = {0};   // bpg_last_statements_stats
 }  // namespace
@@ -685,7 +686,8 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         const int device = g_device;
         const auto t_start = std::chrono::steady_clock::now();
         const uint32_t W = std::max<uint32_t>(1, threads);
-        const uint32_t C = std::min<uint32_t>(16, std::max<uint32_t>(1, W / 2));
+        const uint32_t c_set = g_stmt_consumers.load();
+        const uint32_t C = std::min<uint32_t>(16, std::max<uint32_t>(1, c_set ? c_set : W / 2));
         const size_t label_len = strlen(name);
         const uint8_t *label = (const uint8_t *)name;
         struct Item {
@@ -875,10 +877,13 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         }
         spare.clear();   // the recycled statements' device memory, freed once per call
         {
-            // the bounding stage: the device consumers waited for statements
-            // more than a tenth of their time -> the CPU workers
+            // the bounding stage: the busier of the two (its threads' busy
+            // share of the wall time; the workers' idle time includes each
+            // call's fill and drain)
             const double wall = since_ms(t_start);
-            const int bound = cidle_ms > 0.10 * wall * C ? 1 : 2;
+            const double wbusy = 1.0 - widle_ms / std::max(1e-9, wall * W);
+            const double cbusy = 1.0 - cidle_ms / std::max(1e-9, wall * C);
+            const int bound = wbusy >= cbusy ? 1 : 2;
             const double v[13] = {(double)W, (double)C, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
                                   widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9};
             std::lock_guard<std::mutex> lk(g_ss_mu);
@@ -893,6 +898,11 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         if (n_ok < (int)count) g_err = first_err;   // guarded() cleared it on entry; keep the reason
         return n_ok;
     }, -1);
+}
+int bpg_set_statements_consumers(uint32_t consumers) {
+    if (consumers > 16) return -1;
+    g_stmt_consumers = consumers;
+    return 0;
 }
 int bpg_last_statements_stats(double *out, int n) {
     std::lock_guard<std::mutex> lk(g_ss_mu);

@@ -72,7 +72,8 @@ const char *bpg_last_error(void);
  * (release with free_proof), or NULL if statement k failed. `threads` CPU
  * workers synthesise and upload statements and draw the TranscriptRng
  * streams of up to 8 statements in lockstep; min(16, threads / 2) more
- * threads drive the device, one HIP stream each. Statements in flight are
+ * threads (bpg_set_statements_consumers overrides) drive the device, one HIP
+ * stream each. Statements in flight are
  * capped by HBM (free memory next to the device threads' workspaces, at the
  * footprint of the first prepared statement), and finished statements' device
  * arrays are recycled for the next ones. Returns the number of
@@ -83,13 +84,17 @@ int bpg_prove_statements(const char *name, const char *const *instances,
                          const uint64_t *seeds, uint32_t count, uint32_t threads,
                          struct ProofArtifacts **out);
 
+/* Added: device threads of later bpg_prove_statements calls of the process
+ * (1-16; 0, the default: min(16, threads / 2)). -1 if out of range. */
+int bpg_set_statements_consumers(uint32_t consumers);
+
 /* Added: the last bpg_prove_statements of the process, per stage (ms summed
  * over threads; out[i], i < n <= 13): [0] CPU workers, [1] device consumers,
  * [2] statements in flight allowed, [3] wall ms, [4] synthesis ms, [5]
  * prepare ms (transpose + upload + commitments), [6] TranscriptRng ms, [7]
  * device prove ms, [8] worker idle ms, [9] consumer idle ms, [10] the
- * bounding stage (1 CPU workers: consumers waited for statements more than a
- * tenth of their time; 2 the device consumers), [11] statements in flight
+ * bounding stage, the one whose threads were busy the larger share of the
+ * wall time (1 CPU workers, 2 device consumers), [11] statements in flight
  * HBM admits (sized from the first prepared statement), [12] GB one prepared
  * statement holds. */
 int bpg_last_statements_stats(double *out, int n);
