@@ -495,6 +495,12 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         size_t free_b = 0, total_b = 0;
         BPG_HIP(hipMemGetInfo(&free_b, &total_b));
         const size_t slot_bytes = 2 * (size_t)cs.n * 64 + 64;
+        // RNG slots (2n x 64 B each): every consumer's L proofs, plus groups
+        // of 8 being drawn by at most four producers at a time (four draw
+        // ~100 proofs/s at 2^20, above what the device proves; with 2C slots
+        // for the consumers, as before, CPU-starved producers held slots that
+        // consumers needed for full steps, profiles/r04d_cpus4.json)
+        const uint32_t draw_slots = 8 * std::min<uint32_t>(P, 4);
         const size_t est_c = consumer_bytes_estimate(cs, (int)L);
         const size_t reserve = std::max<size_t>((size_t)2 << 30, total_b / 64) + verifier_bytes_estimate(cs);
         uint32_t C_hbm = 0;
@@ -510,13 +516,13 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                 have_slots = cs.slot_bytes >= slot_bytes ? cs.slot_bufs.size() : 0;
             }
             for (C_hbm = C; C_hbm > 1; C_hbm--) {
-                const size_t want_slots = std::min<size_t>(8 * (size_t)P + 2 * C_hbm, 8 * (size_t)groups);
+                const size_t want_slots = std::min<size_t>(draw_slots + (size_t)L * C_hbm, 8 * (size_t)groups);
                 const size_t new_slots = want_slots > have_slots ? (want_slots - have_slots) * slot_bytes : 0;
                 if ((double)C_hbm * est_c + new_slots + reserve <= (double)free_b + held) break;
             }
         }
         C = std::min(C, C_hbm);
-        const uint32_t nslots = std::min<uint32_t>(8 * P + 2 * C, 8 * groups);
+        const uint32_t nslots = std::min<uint32_t>(draw_slots + L * C, 8 * groups);
         std::vector<uint8_t *> slot = cs.slots(nslots, slot_bytes);
         std::mutex mu;
         std::condition_variable cv;
