@@ -787,7 +787,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         stages = bpg.last_statements_stats()
         if any(o is None for o in outs):
             raise SystemExit("bench: a statement failed: %s" % bpg.last_error())
-        api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(16, max(1, a.consumers or threads // 2)))
+        api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(12 if a.consumers else 8, max(1, a.consumers or threads // 2)))
     if dist is not None:
         dt = D.max_over_ranks(dt)
     last = texts[-1]

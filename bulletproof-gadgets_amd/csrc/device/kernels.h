@@ -52,6 +52,8 @@ ProfSink *prof_sink();
 // (160 B); MSM window rows returned to the host are extended.
 // out[i] = -in[i] (affine Niels: swap y+x / y-x, negate 2dxy)
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st);
+// out[i] = in[i] as affine Niels (cached in; one inversion per 32 points)
+void launch_cached_to_niels(const PtD *in, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = from_uniform_bytes(uniform[64*i .. 64*i+64))
 void launch_gens_map(const uint8_t *uniform, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = v[i]*B + vb[i]*B_blinding using fixed-base tables (64 x 8 points each)

@@ -693,7 +693,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         const auto t_start = std::chrono::steady_clock::now();
         const uint32_t W = std::max<uint32_t>(1, threads);
         const uint32_t c_set = g_stmt_consumers.load();
-        const uint32_t C = std::min<uint32_t>(16, std::max<uint32_t>(1, c_set ? c_set : W / 2));
+        const uint32_t C = std::min<uint32_t>(c_set ? 12 : 8, std::max<uint32_t>(1, c_set ? c_set : W / 2));
         const size_t label_len = strlen(name);
         const uint8_t *label = (const uint8_t *)name;
         struct Item {
@@ -906,7 +906,10 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
     }, -1);
 }
 int bpg_set_statements_consumers(uint32_t consumers) {
-    if (consumers > 16) return -1;
+    // 16 device threads next to 16 workers' upload streams ran the HIP
+    // runtime out of queue resources (HSA_STATUS_ERROR_OUT_OF_RESOURCES,
+    // profiles/r04n_stmts_c16.err); 12 measured slower than 8
+    if (consumers > 12) return -1;
     g_stmt_consumers = consumers;
     return 0;
 }

@@ -1061,6 +1061,7 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // The IPP's c_L Q and c_R Q terms are added on the host (Q = w B, so
 // c Q = (c w) B by the fixed-base table): the L/R jobs hold only generator
 // segments (at most 16 per proof, 32 per job).
+static constexpr bool NIELS_LEVELS = false;   // materialised IPP levels as affine Niels (niels_level)
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms,
                                                      const AllGather *ag, const CommitPre *pre) {
@@ -1328,6 +1329,23 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     bool tail = false;
     uint32_t M = 0;
     uint32_t len = Nl;
+    // A level a fold group materialises (cached points in Gp/Hp[cur]) is
+    // converted to affine Niels in the other buffer (k_cached_to_niels: one
+    // inversion per 32 points, ~15M per point): every later MSM entry over it
+    // is then a 7M madd in pass 1's three-wave kernel instead of an 8M cached
+    // addition at two waves, and the folds read it as they read generators.
+    auto niels_level = [&](uint32_t cnt) {
+        if (!NIELS_LEVELS) return;
+        const int oth = cur == 0 ? 1 : 0;
+        for (int p = 0; p < P; p++) {
+            ProofBufs &B = ws.pb[p];
+            launch_cached_to_niels(as<PtD>(B.Gp[cur]), as<NielsD>(B.Gp[oth]), cnt, st);
+            launch_cached_to_niels(as<PtD>(B.Hp[cur]), as<NielsD>(B.Hp[oth]), cnt, st);
+            Gh[p] = B.Gp[oth].p; Hh[p] = B.Hp[oth].p;
+        }
+        cur = oth;
+        gfmt = MSM_NIELS;
+    };
     // a (= l(x), zero past the real lanes) is nonzero only on lanes < anz:
     // anz = nl, then min(anz, h) after each round's fold
     uint32_t anz = nl;
@@ -1346,10 +1364,11 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             }
         }
         // MSM bases: the level-0 generators (affine Niels), else Ghat/Hhat (cached)
-        const int mfmt = cur < 0 ? MSM_NIELS : MSM_CACHED;
+        const int mfmt = cur < 0 ? MSM_NIELS : gfmt;
         const size_t ps = mfmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
-        // Niels jobs gather negated level-0 generators for negative digits
-        const int64_t gn = mfmt == MSM_NIELS ? gneg : 0;
+        // jobs over the level-0 generators gather their negated copies for
+        // negative digits (a converted level negates in registers)
+        const int64_t gn = cur < 0 ? gneg : 0;
         auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
         const bool lazy = depth == 1;
         const size_t hh = h;
@@ -1415,7 +1434,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                 for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
             }
         }
-        if (mfmt == MSM_NIELS)   // level-0 generator segments gather from the fixed-base tables
+        if (cur < 0)   // level-0 generator segments gather from the fixed-base tables
             for (int i = 0; i < nseg; i++) seg[i].wstride = gws;
         int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt, rowsLR_dev);
@@ -1471,6 +1490,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                 }
                 cur = nxt;
                 gfmt = MSM_CACHED;
+                niels_level(h);
             } else if (depth == 1) {
                 // level k+2 from level k: out_i = P_i + c1 P_{i+h1} + c2 P_{i+2h1} + c3 P_{i+3h1}
                 const uint32_t h1 = h, h0 = 2 * h;
@@ -1521,6 +1541,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                 }
                 cur = nxt;
                 gfmt = MSM_CACHED;
+                niels_level(h);
                 depth = 0;
             } else {
                 // level k+3 from level k: out_i = sum_{t<8} c_t P_{i + t hq}, point
@@ -1563,6 +1584,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
                 }
                 cur = nxt;
                 gfmt = MSM_CACHED;
+                niels_level(h);
                 depth = 0;
             }
         }
@@ -1583,7 +1605,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         launch_from_mont(as<ScD>(B.wG), M, wc, st);
         launch_from_mont(as<ScD>(B.wH), M, wc + M, st);
         MsmSeg sl[2] = {{wc, Gh[0], M, 0}, {wc + M, Hh[0], M, 1}};
-        MsmPlan pl = ws.msm->enqueue(sl, 2, 2, rowsLR, MSM_CACHED);
+        MsmPlan pl = ws.msm->enqueue(sl, 2, 2, rowsLR, gfmt);
         ws.sync();
         combine_rows(Gfin, rowsLR, pl.W, pl.c);
         combine_rows(Hfin, rowsLR + pl.W, pl.W, pl.c);

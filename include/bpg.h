@@ -71,7 +71,7 @@ const char *bpg_last_error(void);
  * seeds == NULL: OS entropy), and out[k] receives what that c_prove returns
  * (release with free_proof), or NULL if statement k failed. `threads` CPU
  * workers synthesise and upload statements and draw the TranscriptRng
- * streams of up to 8 statements in lockstep; min(16, threads / 2) more
+ * streams of up to 8 statements in lockstep; min(8, threads / 2) more
  * threads (bpg_set_statements_consumers overrides) drive the device, one HIP
  * stream each. Statements in flight are
  * capped by HBM (free memory next to the device threads' workspaces, at the
@@ -85,7 +85,7 @@ int bpg_prove_statements(const char *name, const char *const *instances,
                          struct ProofArtifacts **out);
 
 /* Added: device threads of later bpg_prove_statements calls of the process
- * (1-16; 0, the default: min(16, threads / 2)). -1 if out of range. */
+ * (1-12; 0, the default: min(8, threads / 2)). -1 if out of range. */
 int bpg_set_statements_consumers(uint32_t consumers);
 
 /* Added: the last bpg_prove_statements of the process, per stage (ms summed
