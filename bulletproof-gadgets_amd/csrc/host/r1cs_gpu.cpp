@@ -1061,7 +1061,6 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // The IPP's c_L Q and c_R Q terms are added on the host (Q = w B, so
 // c Q = (c w) B by the fixed-base table): the L/R jobs hold only generator
 // segments (at most 16 per proof, 32 per job).
-static constexpr bool NIELS_LEVELS = false;   // materialised IPP levels as affine Niels (niels_level)
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms,
                                                      const AllGather *ag, const CommitPre *pre) {
@@ -1333,9 +1332,9 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     // converted to affine Niels in the other buffer (k_cached_to_niels: one
     // inversion per 32 points, ~15M per point): every later MSM entry over it
     // is then a 7M madd in pass 1's three-wave kernel instead of an 8M cached
-    // addition at two waves, and the folds read it as they read generators.
+    // addition at two waves, and the folds read it as they read generators
+    // (+0.9% in the bench, profiles/r04o_ab.txt).
     auto niels_level = [&](uint32_t cnt) {
-        if (!NIELS_LEVELS) return;
         const int oth = cur == 0 ? 1 : 0;
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
