@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-4 record: smoke, the whole GPU suite, then the driver's bench command.
+set -o pipefail
+mkdir -p gpurun_out
+R=${1:-r04p}
+timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${R}_smoke.log 2>&1 &&
+timeout -k 10 720 python -u -m pytest tests -m gpu -v --maxfail=3 --timeout 300 --timeout-method thread \
+    > gpurun_out/${R}_gpu_tests.log 2>&1 &&
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err
+echo "rc=$?"
