@@ -55,8 +55,12 @@ def parse():
                          "Default: producers + 8 (verify mode 24)")
     ap.add_argument("--producers", type=int, default=0,
                     help="TranscriptRng producer threads per GPU (default: one per CPU of the rank's share, at most 8)")
+    ap.add_argument("--ipp-tail", type=int, default=-1,
+                    help="IPP tail threshold in lanes (bpg_ctx_set_ipp_tail; -1: the default, 4096)")
     ap.add_argument("--consumers", type=int, default=0,
-                    help="statements mode: device threads (bpg_set_statements_consumers; 0: threads / 2)")
+                    help="statements mode: device threads (bpg_set_statements_layout; 0: min(5, threads / 2))")
+    ap.add_argument("--stmt-lockstep", type=int, default=0,
+                    help="statements mode: statements a device thread proves at once (1-4; 0: 4)")
     ap.add_argument("--max-inflight", type=int, default=0,
                     help="proofs in flight per GPU (bpg_ctx_set_pipeline max_inflight; 0: 24 at 2^20, and what HBM "
                          "admits)")
@@ -368,8 +372,8 @@ def main():
     bpg.set_seed(1000 + srank)
     syn = bpg.Synth(inst, wit, gad)
     ctx = bpg.Context(dev)
-    if a.fold_tables >= 0 or a.msm_tables >= 0:
-        ctx.set_strategy(fold_tables=a.fold_tables, msm_tables=a.msm_tables)
+    if a.fold_tables >= 0 or a.msm_tables >= 0 or a.ipp_tail >= 0:
+        ctx.set_strategy(fold_tables=a.fold_tables, ipp_tail=a.ipp_tail, msm_tables=a.msm_tables)
     ctx.set_pipeline(producers=min(producers, 8), max_inflight=a.max_inflight)
     if a.mode == "latency":
         return bench_latency(a, bpg, ctx, syn, D, dist, rank, world, W)
@@ -515,7 +519,8 @@ def main():
                    "parallelism": "independent proofs per GPU (%d ranks)" % world,
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
                    "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables],
-                   "msm_fixed_base_tables": {-1: "default (off)", 0: "off", 1: "on"}[a.msm_tables]},
+                   "msm_fixed_base_tables": {-1: "default (off)", 0: "off", 1: "on"}[a.msm_tables],
+                   "ipp_tail_lanes": a.ipp_tail if a.ipp_tail >= 0 else "default (4096)"},
         "host_cores_busy": round(host_busy, 2),
         # the producer/consumer pipeline of the timed batch (bpg_last_batch_stats):
         # consumer time starved of ready proofs while producers were drawing
@@ -777,7 +782,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         api = "c_prove on %d threads" % threads
         stages = None
     else:   # bpg_prove_statements: lockstep RNG over distinct statements, device consumers
-        bpg.set_statements_consumers(a.consumers)
+        bpg.set_statements_layout(a.consumers, a.stmt_lockstep)
         bpg.prove_statements("bench", texts[:batch * a.warmup], threads)
         barrier()
         t0 = time.perf_counter()
@@ -787,7 +792,9 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         stages = bpg.last_statements_stats()
         if any(o is None for o in outs):
             raise SystemExit("bench: a statement failed: %s" % bpg.last_error())
-        api = "bpg_prove_statements, %d CPU workers + %d device threads" % (threads, min(12 if a.consumers else 8, max(1, a.consumers or threads // 2)))
+        api = "bpg_prove_statements, %d CPU workers + %d device threads of up to %d statements" % (
+            threads, stages["consumers"] if stages else min(12 if a.consumers else 5, max(1, a.consumers or threads // 2)),
+            a.stmt_lockstep or 4)
     if dist is not None:
         dt = D.max_over_ranks(dt)
     last = texts[-1]

@@ -33,7 +33,7 @@ EXPORTS = [
     "bpg_cs_merkle_tree", "bpg_cs_range_proof", "bpg_cs_view", "bpg_cs_V", "bpg_prepare_shard",
     "bpg_prove_prepared", "bpg_verify_prepared", "bpg_ctx_trim", "bpg_prove_statements",
     "bpg_ctx_set_pipeline", "bpg_last_batch_stats", "bpg_last_statements_stats", "bpg_ctx_set_msm_tables",
-    "bpg_set_statements_consumers",
+    "bpg_set_statements_layout",
 ]
 
 # bpg_allgather_fn (include/bpg.h)
@@ -99,7 +99,7 @@ def lib():
         L.bpg_ctx_set_msm_tables.argtypes = [vp, ctypes.c_int]
         L.bpg_last_batch_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.bpg_last_statements_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
-        L.bpg_set_statements_consumers.argtypes = [u32]
+        L.bpg_set_statements_layout.argtypes = [u32, u32]
         L.bpg_r1cs_prove_sharded.argtypes = [vp, vp, sz, vp, vp, u32, u32, ALLGATHER_FN, vp, vp, sz,
                                              ctypes.POINTER(sz), vp]
         L.bpg_prepare.restype = vp
@@ -182,11 +182,12 @@ def prove(name, instance, witness, gadgets):
     return proof, coms
 
 
-def set_statements_consumers(consumers):
-    """bpg_set_statements_consumers: device threads of later
-    prove_statements calls (0: threads / 2)."""
-    if lib().bpg_set_statements_consumers(consumers) != 0:
-        raise BpgError("statements consumers out of range")
+def set_statements_layout(consumers=0, lockstep=0):
+    """bpg_set_statements_layout: device threads of later prove_statements
+    calls (0: min(5, threads / 2), capped by HBM) and statements each proves
+    at once (0: 4)."""
+    if lib().bpg_set_statements_layout(consumers, lockstep) != 0:
+        raise BpgError("statements layout out of range")
 
 
 def prove_statements(name, statements, threads, seeds=None):

@@ -677,7 +677,7 @@ static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector
     return a;
 }
 namespace {
-std::atomic<uint32_t> g_stmt_consumers(0);   // bpg_set_statements_consumers (0: threads / 2)
+std::atomic<uint32_t> g_stmt_consumers(0), g_stmt_lockstep(0);   // bpg_set_statements_layout (0: defaults)
 std::mutex g_ss_mu;
 double g_ss[13] = {0};   // bpg_last_statements_stats
 }  // namespace
@@ -693,7 +693,12 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         const auto t_start = std::chrono::steady_clock::now();
         const uint32_t W = std::max<uint32_t>(1, threads);
         const uint32_t c_set = g_stmt_consumers.load();
-        const uint32_t C = std::min<uint32_t>(c_set ? 12 : 8, std::max<uint32_t>(1, c_set ? c_set : W / 2));
+        // device threads, each proving up to L ready statements of one shape
+        // in lockstep (one MSM job per IPP round for all of them, as
+        // bpg_prove_batch does for one circuit)
+        const uint32_t l_set = g_stmt_lockstep.load();
+        const uint32_t L = l_set ? l_set : 4;
+        const uint32_t C = std::min<uint32_t>(c_set ? 12 : 5, std::max<uint32_t>(1, c_set ? c_set : W / 2));
         const size_t label_len = strlen(name);
         const uint8_t *label = (const uint8_t *)name;
         struct Item {
@@ -727,7 +732,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         // (profiles/r04d_statements.json). At most 4W + 8 + 2C, and at most
         // what HBM holds next to the consumers' workspaces, sized once the
         // first statement is prepared (until then at most W)
-        uint32_t limit = 4 * W + 8 + 2 * C, hbm_limit = 0;
+        uint32_t limit = 4 * W + 8 + 2 * C, hbm_limit = 0, C_eff = C;
         double est_st = 0;
         double synth_ms = 0, prep_ms = 0, rng_ms = 0, prove_ms = 0, widle_ms = 0, cidle_ms = 0;
         std::string first_err;
@@ -743,7 +748,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             const bool worker = (uint32_t)id < W;
             for (;;) {
                 std::vector<std::unique_ptr<Item>> group;
-                std::unique_ptr<Item> item;
+                std::vector<std::unique_ptr<Item>> items;   // a consumer's lockstep step
                 std::unique_ptr<PreparedCS> reuse;
                 uint32_t k = 0;
                 int what = 0;   // 1 synthesise k, 2 RNG group, 3 device
@@ -752,16 +757,28 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     const auto tw = std::chrono::steady_clock::now();
                     cv.wait(lk, [&] {
                         if (fatal || done == count) return true;
-                        if (!worker) return !ready.empty();
+                        if (!worker) return (uint32_t)id - W >= C_eff || !ready.empty();
                         const bool tail = next == count && synth_busy == 0;
                         if (prepared.size() >= 8 || (tail && !prepared.empty())) return true;
                         return next < count && inflight < (est_st > 0 ? limit : W);
                     });
+                    if (!worker && (uint32_t)id - W >= C_eff) break;   // not admitted by HBM
                     (worker ? widle_ms : cidle_ms) += since_ms(tw);
                     if (fatal || done == count) break;
                     if (!worker) {
-                        item = std::move(ready.front());
+                        items.push_back(std::move(ready.front()));
                         ready.pop_front();
+                        // up to L - 1 more ready statements of the same shape
+                        const PreparedCS &c0 = *items[0]->cs;
+                        for (auto it = ready.begin(); it != ready.end() && items.size() < L;) {
+                            const PreparedCS &c = *(*it)->cs;
+                            if (c.n == c0.n && c.m == c0.m && c.N == c0.N) {
+                                items.push_back(std::move(*it));
+                                it = ready.erase(it);
+                            } else {
+                                ++it;
+                            }
+                        }
                         what = 3;
                     } else if (prepared.size() >= 8 || (next == count && synth_busy == 0 && !prepared.empty())) {
                         while (!prepared.empty() && group.size() < 8) {
@@ -815,14 +832,26 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     synth_ms += ms_s;
                     prep_ms += ms_p;
                     if (ok && est_st == 0) {
-                        // HBM budget of statements in flight: free memory and
-                        // the consumers' reusable workspaces, less C
-                        // one-proof workspaces and a reserve
+                        // HBM budget, sized from the first prepared statement:
+                        // free memory and the consumers' reusable workspaces,
+                        // less a reserve, must hold C_eff consumer workspaces
+                        // of L proofs and at least C_eff L + 8 statements in
+                        // flight (the rest of it bounds the in-flight limit);
+                        // consumers beyond C_eff stay idle
                         est_st = (double)prepared_bytes(*it->cs);
                         const double reserve = std::max<double>(2.0 * (1 << 30), total_b / 64.0);
-                        const double avail = (double)free_b + (double)held - reserve -
-                                             (double)C * (double)consumer_bytes_estimate(*it->cs, 1);
-                        hbm_limit = (uint32_t)std::max<double>(std::min<double>(C + 8, limit), avail / est_st);
+                        const double per_c = (double)consumer_bytes_estimate(*it->cs, (int)L);
+                        // free memory now: the first prepare built the comb
+                        // tables (208 GB at 2^20) if no earlier call had;
+                        // this statement's own bytes count as in flight
+                        size_t free_now = 0, tot_now = 0;
+                        BPG_HIP(hipMemGetInfo(&free_now, &tot_now));
+                        const double all = (double)free_now + (double)held + est_st - reserve;
+                        uint32_t c_fit = C;
+                        while (c_fit > 1 && c_fit * per_c + (c_fit * L + 8) * est_st > all) c_fit--;
+                        C_eff = c_fit;
+                        hbm_limit = (uint32_t)std::max<double>(std::min<double>(C_eff * L + 8, limit),
+                                                               (all - C_eff * per_c) / est_st);
                         limit = std::min(limit, hbm_limit);
                     }
                     if (ok) prepared.push_back(std::move(it));
@@ -853,23 +882,28 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                     cv.notify_all();
                 } else {
                     const auto t0 = std::chrono::steady_clock::now();
+                    const int P = (int)items.size();
                     try {
-                        std::vector<uint8_t> pr = gpu_prove_rng(*item->cs, label, label_len, item->rb);
-                        out[item->k] = make_artifacts(item->coms, pr);
+                        const PreparedCS *csv[MAX_LOCKSTEP];
+                        const RngBlock *rbs[MAX_LOCKSTEP];
+                        for (int i = 0; i < P; i++) { csv[i] = items[i]->cs.get(); rbs[i] = &items[i]->rb; }
+                        std::vector<std::vector<uint8_t>> prs = gpu_prove_lockstep(csv, label, label_len, rbs, P, nullptr);
+                        for (int i = 0; i < P; i++) out[items[i]->k] = make_artifacts(items[i]->coms, prs[i]);
                         std::lock_guard<std::mutex> lk(mu);
-                        proved++;
+                        proved += P;
                     } catch (const dev::HipError &e) {
-                        note_err(item->k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr, true);
+                        note_err(items[0]->k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr,
+                                 true);
                     } catch (const std::exception &e) {
-                        note_err(item->k, e.what(), false);
+                        note_err(items[0]->k, e.what(), false);
                     }
                     const double ms = since_ms(t0);
                     std::lock_guard<std::mutex> lk(mu);
                     prove_ms += ms;
-                    spare.push_back(std::move(item->cs));   // recycled by the next statement
-                    item.reset();
-                    inflight--;
-                    done++;
+                    for (auto &it : items) spare.push_back(std::move(it->cs));   // recycled by the next statements
+                    items.clear();
+                    inflight -= P;
+                    done += P;
                     cv.notify_all();
                 }
             }
@@ -888,9 +922,9 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             // call's fill and drain)
             const double wall = since_ms(t_start);
             const double wbusy = 1.0 - widle_ms / std::max(1e-9, wall * W);
-            const double cbusy = 1.0 - cidle_ms / std::max(1e-9, wall * C);
+            const double cbusy = 1.0 - cidle_ms / std::max(1e-9, wall * C_eff);
             const int bound = wbusy >= cbusy ? 1 : 2;
-            const double v[13] = {(double)W, (double)C, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
+            const double v[13] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
                                   widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9};
             std::lock_guard<std::mutex> lk(g_ss_mu);
             memcpy(g_ss, v, sizeof(v));
@@ -905,12 +939,13 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         return n_ok;
     }, -1);
 }
-int bpg_set_statements_consumers(uint32_t consumers) {
+int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep) {
     // 16 device threads next to 16 workers' upload streams ran the HIP
     // runtime out of queue resources (HSA_STATUS_ERROR_OUT_OF_RESOURCES,
-    // profiles/r04n_stmts_c16.err); 12 measured slower than 8
-    if (consumers > 12) return -1;
+    // profiles/r04n_stmts_c16.err)
+    if (consumers > 12 || lockstep > (uint32_t)MAX_LOCKSTEP) return -1;
     g_stmt_consumers = consumers;
+    g_stmt_lockstep = lockstep;
     return 0;
 }
 int bpg_last_statements_stats(double *out, int n) {
@@ -920,9 +955,10 @@ int bpg_last_statements_stats(double *out, int n) {
 }
 
 // Verifier::verify (verify.rs:71) over `count` proofs of one prepared
-// circuit: each worker thread verifies whole proofs on its own HIP stream
-// (proofs are independent; the sharded single-proof path is
-// bpg_r1cs_verify_shard). results[k] = 1 accept, 0 reject.
+// circuit: the proofs are cut into one chunk per worker thread (8 to 64
+// proofs each), and each thread checks its chunk with one random-linear-
+// combination MSM on its own HIP stream (gpu_verify_batch; a chunk that
+// fails is re-verified proof by proof). results[k] = 1 accept, 0 reject.
 int bpg_verify_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, const uint8_t *V,
                      const uint8_t *proofs, size_t proof_stride, const size_t *lens, uint32_t count,
                      uint32_t threads, const uint8_t entropy[32], int *results) {
@@ -932,21 +968,24 @@ int bpg_verify_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, co
         // the prover's layout drops the constant column the verifier needs
         if (cs.prover) throw std::runtime_error("circuit prepared for proving: use bpg_prepare_verifier");
         if (threads == 0) threads = 1;
-        threads = std::min<uint32_t>(threads, count);
+        const uint32_t chunk = std::min<uint32_t>(64, std::max<uint32_t>(8, (count + threads - 1) / threads));
+        const uint32_t nchunks = (count + chunk - 1) / chunk;
+        threads = std::min<uint32_t>(threads, nchunks);
         std::atomic<uint32_t> next(0);
         std::mutex mu;
         std::string err;
         pool().run((int)threads, [&](int) {
             try {
                 for (;;) {
-                    const uint32_t k = next.fetch_add(1);
-                    if (k >= count) break;
+                    const uint32_t c = next.fetch_add(1);
+                    if (c >= nchunks) break;
                     {
                         std::lock_guard<std::mutex> lk(mu);
                         if (!err.empty()) break;
                     }
-                    results[k] = gpu_verify(cs, label, label_len, V, proofs + proof_stride * (size_t)k, lens[k],
-                                            entropy);
+                    const uint32_t k0 = c * chunk, k1 = std::min(count, k0 + chunk);
+                    gpu_verify_batch(cs, label, label_len, V, proofs + proof_stride * (size_t)k0, proof_stride,
+                                     lens + k0, k1 - k0, entropy, results + k0);
                 }
             } catch (const dev::HipError &e) {
                 std::lock_guard<std::mutex> lk(mu);

@@ -336,7 +336,6 @@ void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_st
 // ---------------------------------------------------------------- workspace
 // Per-proof device buffers of the prover: a workspace drives up to
 // MAX_LOCKSTEP proofs of one circuit in lockstep (gpu_prove_lockstep).
-static const int MAX_LOCKSTEP = 4;
 static const size_t ROWS_HALF = 1024;   // pinned MSM row buffer: commitments [0, 1024), IPP L/R [1024, 2048)
 struct ProofBufs {
     DBuf wide, sL, sR, w, wloc, l1, r0, r1, r3, ypm, yipm, zlo, zhi, ylo, yhi, tabs, a, b, mscal, partial, Gp[2], Hp[2],
@@ -361,7 +360,7 @@ struct Workspace : dev::ProfSink {
     int device = 0;
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
-    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag;
+    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag, ghacc, vcomp;
     PtD *rows_host = nullptr;        // pinned, 2 x ROWS_HALF window rows
     PtD *rows_view = nullptr;        // its device view (the row kernels write there)
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
@@ -378,7 +377,8 @@ struct Workspace : dev::ProfSink {
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
-        DBuf *bufs[] = {&w, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs, &mscal, &partial, &small, &gh, &ynwR, &pts, &okflag};
+        DBuf *bufs[] = {&w, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs, &mscal, &partial, &small, &gh, &ynwR, &pts, &okflag,
+                        &ghacc, &vcomp};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -470,7 +470,7 @@ size_t thread_workspace_bytes(int device) {
     const Workspace &ws = *it->second;
     size_t b = ws.msm ? ws.msm->bytes() : 0;
     for (const DBuf *d : {&ws.w, &ws.yipm, &ws.zlo, &ws.zhi, &ws.ylo, &ws.yhi, &ws.tabs, &ws.mscal, &ws.partial,
-                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag})
+                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag, &ws.ghacc, &ws.vcomp})
         b += d->cap;
     for (const ProofBufs &B : ws.pb)
         for (const DBuf *d : {&B.wide, &B.sL, &B.sR, &B.w, &B.wloc, &B.l1, &B.r0, &B.r1, &B.r3, &B.ypm, &B.yipm,
@@ -1061,11 +1061,29 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // The IPP's c_L Q and c_R Q terms are added on the host (Q = w B, so
 // c Q = (c w) B by the fixed-base table): the L/R jobs hold only generator
 // segments (at most 16 per proof, 32 per job).
+// Proof p's circuit is csv[p]: one prepared circuit for the proofs of a
+// batch, or distinct statements of one shape (n, m, N: the IPP and every
+// MSM job depend only on those; a_L/a_R/a_O, the constraint matrix and the
+// commitments are each proof's own).
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms,
                                                      const AllGather *ag, const CommitPre *pre) {
-    if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
+    const PreparedCS *csv[MAX_LOCKSTEP];
+    for (int p = 0; p < MAX_LOCKSTEP; p++) csv[p] = &cs;
+    return gpu_prove_lockstep(csv, label, label_len, rbs, P, tms, ag, pre);
+}
+std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *csv, const uint8_t *label,
+                                                     size_t label_len, const RngBlock *const *rbs, int P,
+                                                     ProveTimings *tms, const AllGather *ag, const CommitPre *pre) {
     if (P < 1 || P > MAX_LOCKSTEP) throw std::runtime_error("lockstep proof count");
+    const PreparedCS &cs = *csv[0];
+    for (int p = 0; p < P; p++) {
+        const PreparedCS &c = *csv[p];
+        if (!c.prover) throw std::runtime_error("prepared circuit has no witness");
+        if (c.n != cs.n || c.m != cs.m || c.N != cs.N || c.world != cs.world || c.rank != cs.rank ||
+            c.device != cs.device)
+            throw std::runtime_error("lockstep proofs of different shapes");
+    }
     static_assert(16 * MAX_LOCKSTEP <= MSM_MAX_SEGS, "an IPP job holds up to 16 segments per proof");
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t n = cs.n, m = cs.m, N = cs.N, lgN = cs.lgN;
@@ -1087,7 +1105,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             BPG_HIP(hipHostMalloc((void **)&B.small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
             BPG_HIP(hipHostGetDevicePointer((void **)&B.small_view, B.small_host, 0));
         }
-        T.push_back(prover_transcript(cs, label, label_len));
+        T.push_back(prover_transcript(*csv[p], label, label_len));
     }
 
     // A_I1 = <a_L,G> + <a_R,H>, A_O1 = <a_O,G>, S1 = <s_L,G> + <s_R,H>
@@ -1128,9 +1146,10 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             }
             launch_wide_reduce(wd, nl, world, rank, as<ScD>(B.sL), st);
             launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(B.sR), st);
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg, gws};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg, gws};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws};
+            const PreparedCS &cp = *csv[p];
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cp.aL)), G0, nl, 0, gneg, gws};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cp.aR)), H0, nl, 0, gneg, gws};
+            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cp.aO)), G0, nl, 1, gneg, gws};
             seg[nseg++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
             seg[nseg++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};
         }
@@ -1186,11 +1205,12 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
     // vectors: powers, flattened_constraints(z), l(x)/r(x) coefficients, t(x)
     // (y^i and y^-i at this rank's lanes: (y^world)^j * y^rank)
     std::vector<Scalar> y_inv(P);
-    CscDev csc{as<uint32_t>(const_cast<DBuf &>(cs.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cs.col_row)),
-               as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
-               as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
     for (int p = 0; p < P; p++) {
         ProofBufs &B = ws.pb[p];
+        const PreparedCS &cp = *csv[p];
+        CscDev csc{as<uint32_t>(const_cast<DBuf &>(cp.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cp.col_row)),
+                   as<ScD>(const_cast<DBuf &>(cp.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cp.short_cols)),
+                   as<uint32_t>(const_cast<DBuf &>(cp.long_cols)), cp.nshort, cp.nlong, cp.ncol, 3 * n};
         y_inv[p] = sc_invert(y[p]);
         B.ypm.grow((size_t)Nl * sizeof(ScD));
         B.yipm.grow((size_t)Nl * sizeof(ScD));
@@ -1200,13 +1220,13 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         // synchronise the whole device, every other stream included
         pow_vector(B.small_host, B.tabs, st, 2, sharded ? sc_pow_u64(y_inv[p], world) : y_inv[p], Nl, B.ylo, B.yhi,
                    as<ScD>(B.yipm), sharded ? sc_pow_u64(y_inv[p], rank) : Scalar::one());
-        pow_vector(B.small_host, B.tabs, st, 4, z[p], cs.q + 2, B.zlo, B.zhi, nullptr);
-        B.w.grow((size_t)cs.ncol * sizeof(ScD) + 64);
-        int pfl = ws.prof_begin("flatten", (double)cs.ncol * 32);
+        pow_vector(B.small_host, B.tabs, st, 4, z[p], cp.q + 2, B.zlo, B.zhi, nullptr);
+        B.w.grow((size_t)cp.ncol * sizeof(ScD) + 64);
+        int pfl = ws.prof_begin("flatten", (double)cp.ncol * 32);
         launch_flatten(csc, as<ScD>(B.zlo), as<ScD>(B.zhi), as<ScD>(B.w), st);
         B.partial.grow(1024 * 8 * sizeof(ScD));
-        for (uint32_t col : cs.huge_cols)
-            launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(B.zlo),
+        for (uint32_t col : cp.huge_cols)
+            launch_flatten_huge(csc, col, cp.col_ptr_host[col], cp.col_ptr_host[col + 1], as<ScD>(B.zlo),
                                 as<ScD>(B.zhi), as<ScD>(B.partial), as<ScD>(B.w), st);
         ws.prof_end(pfl);
         ScD *wfull = as<ScD>(B.w);
@@ -1223,15 +1243,15 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         B.small.grow(64 * sizeof(ScD));
         ScD *dsmall = B.small_view + 1000;   // t_1..t_6, <w_V, v_blinding> (pinned, device view)
         if (nl) {
-            launch_lr_build(as<ScD>(const_cast<DBuf &>(cs.aL)), as<ScD>(const_cast<DBuf &>(cs.aR)), as<ScD>(B.sR), wL,
+            launch_lr_build(as<ScD>(const_cast<DBuf &>(cp.aL)), as<ScD>(const_cast<DBuf &>(cp.aR)), as<ScD>(B.sR), wL,
                             wR, wO, as<ScD>(B.ypm), as<ScD>(B.yipm), nl, as<ScD>(B.l1), as<ScD>(B.r0), as<ScD>(B.r1),
                             as<ScD>(B.r3), st);
-            launch_tpoly(as<ScD>(B.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(B.sL), as<ScD>(B.r0),
+            launch_tpoly(as<ScD>(B.l1), as<ScD>(const_cast<DBuf &>(cp.aO)), as<ScD>(B.sL), as<ScD>(B.r0),
                          as<ScD>(B.r1), as<ScD>(B.r3), nl, as<ScD>(B.partial), dsmall, st);
         } else {
             BPG_HIP(hipMemsetAsync(dsmall, 0, 6 * sizeof(ScD), st));
         }
-        if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cs.vb_dev)), m, as<ScD>(B.partial), dsmall + 6, st);
+        if (m) launch_dot(wV, as<ScD>(const_cast<DBuf &>(cp.vb_dev)), m, as<ScD>(B.partial), dsmall + 6, st);
         else BPG_HIP(hipMemsetAsync(dsmall + 6, 0, sizeof(ScD), st));
     }
     ws.sync();
@@ -1277,7 +1297,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         wch[p] = T[p].challenge_scalar("w");
         B.a.grow((size_t)Nl * sizeof(ScD) + 64);
         B.b.grow((size_t)Nl * sizeof(ScD) + 64);
-        launch_lr_eval(as<ScD>(B.l1), as<ScD>(const_cast<DBuf &>(cs.aO)), as<ScD>(B.sL), as<ScD>(B.r0),
+        launch_lr_eval(as<ScD>(B.l1), as<ScD>(const_cast<DBuf &>(csv[p]->aO)), as<ScD>(B.sL), as<ScD>(B.r0),
                        as<ScD>(B.r1), as<ScD>(B.r3), as<ScD>(B.ypm), nl, Nl, mont(xx), mont(xx * xx), as<ScD>(B.a),
                        as<ScD>(B.b), st);
     }
@@ -1440,6 +1460,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
         ws.prof_end(ph);
         ws.sync();
         std::vector<std::array<Scalar, 4>> rnow(P);   // this round's fold scalars (G a/b, H a/b)
+        ScD *fa[MAX_LOCKSTEP], *fb[MAX_LOCKSTEP], fu[MAX_LOCKSTEP], fui[MAX_LOCKSTEP];   // a, b folds
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             Point LR[2], cq;
@@ -1461,19 +1482,24 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const
             T[p].append_point("R", cr);
             const Scalar uk = T[p].challenge_scalar("u");
             const Scalar uinv = sc_invert(uk);
-            launch_ipp_fold_scalars(as<ScD>(B.a), as<ScD>(B.b), h, mont(uk), mont(uinv), st);
+            fa[p] = as<ScD>(B.a); fb[p] = as<ScD>(B.b); fu[p] = mont(uk); fui[p] = mont(uinv);
             const Scalar u2 = uk * uk, ui2 = uinv * uinv;
             const Scalar yh = sc_pow_u64(y_inv[p], (uint64_t)h * world);   // the round's global half length
             rnow[p] = {u2, u2 * u[p], ui2 * yh, ui2 * yh * u[p]};
             lam[p] = lam[p] * uinv;
             mu[p] = mu[p] * uk;
         }
+        launch_ipp_fold_scalars(fa, fb, fu, fui, P, h, st);   // the round's a, b folds of every proof
         const int nxt = cur == 0 ? 1 : 0;
         if (tail) {
-            if (h > 1 || sharded)
-                for (int p = 0; p < P; p++)
-                    launch_ipp_tail_weights(as<ScD>(ws.pb[p].wG), as<ScD>(ws.pb[p].wH), M, h, nl, mont(rnow[p][0]),
-                                            mont(rnow[p][1]), mont(rnow[p][2]), mont(rnow[p][3]), st);
+            if (h > 1 || sharded) {
+                ScD *wg[MAX_LOCKSTEP], *wh[MAX_LOCKSTEP], rw[MAX_LOCKSTEP][4];
+                for (int p = 0; p < P; p++) {
+                    wg[p] = as<ScD>(ws.pb[p].wG); wh[p] = as<ScD>(ws.pb[p].wH);
+                    for (int q = 0; q < 4; q++) rw[p][q] = mont(rnow[p][q]);
+                }
+                launch_ipp_tail_weights(wg, wh, rw, P, M, h, nl, st);
+            }
         } else if (h > 1) {
             const int group = (comb && cur < 0) ? 2 : group_cfg;
             if (depth + 1 < group) {   // level k + depth + 1 stays implicit
@@ -1711,18 +1737,24 @@ int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, con
     return gpu_verify_shard(cs, label, label_len, V, proof, plen, entropy, 0, 1, nullptr);
 }
 
-// One shard of Verifier::verify's mega-check. Every shard replays the
-// transcript and the rejection checks; shard s of S sums the generator terms
-// j in [s N/S, (s+1) N/S) of G and H, shard 0 also the proof/commitment
-// points and the B, B_blinding terms. The shards' partial sums add up to the
-// point that must be the identity; `partial` (32 B, compressed) receives this
-// shard's part. Returns 1 (partial written, or accept when S == 1), 0 reject.
-int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
-                     const uint8_t *proof, size_t plen, const uint8_t entropy[32], uint32_t shard, uint32_t nshards,
-                     uint8_t *partial) {
-    if (nshards < 1 || shard >= nshards) throw std::runtime_error("bad shard");
-    DeviceContext &ctx = DeviceContext::get(cs.device);
+// The per-proof part of Verifier::verify (verify.rs:71): parse the proof,
+// replay the transcript, and build the verification scalars. The 2N
+// generator scalars land in `gh` (device, canonical: g_0..g_{N-1}, then
+// h_0..h_{N-1}); the proof's ns small points (A_I1, A_O1, S1, V_i, T_*,
+// L_k, R_k) are decompressed to `pts` (an invalid encoding clears *ok_dev)
+// and their scalars, with those of B and B_blinding, go to `vt`. Ends with
+// the stream synchronised and *ok_host holding the decompression verdict.
+// Returns 0 when a format or transcript check rejects the proof.
+struct VerifyTerms {
+    uint32_t ns = 0;
+    std::vector<Scalar> ss;   // scalars of the small points
+    Scalar sB, sBb;           // of B and B_blinding
+};
+static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                        const uint8_t *proof, size_t plen, const uint8_t entropy[32], Workspace &ws, ScD *gh,
+                        NielsD *pts, int *ok_dev, int *ok_host, VerifyTerms &vt) {
     const uint32_t n = cs.n, m = cs.m, N = cs.N;
+    hipStream_t st = ws.st;
     // R1CSProof::from_bytes
     if (plen < 1 || proof[0] != 0) return 0;
     const uint8_t *p = proof + 1;
@@ -1740,9 +1772,6 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     if (lgn >= 32) return 0;
     if (!Scalar::from_canonical(ipp + 64 * lgn, pa) || !Scalar::from_canonical(ipp + 64 * lgn + 32, pb)) return 0;
     if (N != (1u << lgn)) return 0;
-    std::shared_ptr<const GenSet> gs = ctx.gens(N, 0, 1, true);
-    Workspace &ws = thread_workspace(cs.device);
-    hipStream_t st = ws.st;
     ws.tabs.grow(8 * 40 * sizeof(ScD));
     auto is_zero32 = [](const uint8_t *b) { uint8_t a = 0; for (int i = 0; i < 32; i++) a |= b[i]; return a == 0; };
 
@@ -1811,10 +1840,9 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     ws.small.grow(64 * sizeof(ScD) + 4096 * sizeof(ScD));
     ScD *u2d = as<ScD>(ws.small);
     if (lgn) BPG_HIP(hipMemcpyAsync(u2d, u2h, lgn * sizeof(ScD), hipMemcpyHostToDevice, st));
-    ws.gh.grow((size_t)2 * N * sizeof(ScD) + 64);
     ws.ynwR.grow((size_t)(n ? n : 1) * sizeof(ScD) + 64);
     launch_verify_gh(as<ScD>(ws.w), as<ScD>(ws.yipm), u2d, to_dev(allinv), n, N, lgn, mont(x), mont(pa), mont(pb),
-                     mont(u), as<ScD>(ws.gh), as<ScD>(ws.ynwR), st);
+                     mont(u), gh, as<ScD>(ws.ynwR), st);
     ws.partial.grow(1024 * 8 * sizeof(ScD));
     ScD *dsm = u2d + 40;
     if (n) launch_dot(as<ScD>(ws.ynwR), as<ScD>(ws.w), n, as<ScD>(ws.partial), dsm, st);
@@ -1835,28 +1863,59 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
         memcpy(comp.data() + (8 + m + k) * (size_t)32, ipp + 64 * k, 32);
         memcpy(comp.data() + (8 + m + lgn + k) * (size_t)32, ipp + 64 * k + 32, 32);
     }
-    ws.pts.grow(2 * (size_t)ns * sizeof(NielsD) + 64);   // points, then their negations
-    ws.okflag.grow(64);
-    ws.mscal.grow((size_t)ns * 32 + (size_t)ns * sizeof(ScD) + 64);
-    uint32_t *compd = as<uint32_t>(ws.mscal);
-    ScD *sscal = reinterpret_cast<ScD *>(as<uint8_t>(ws.mscal) + (size_t)ns * 32);
+    ws.vcomp.grow((size_t)ns * 32 + 64);
+    uint32_t *compd = as<uint32_t>(ws.vcomp);
     BPG_HIP(hipMemcpyAsync(compd, comp.data(), comp.size(), hipMemcpyHostToDevice, st));
-    int one = 1;
-    BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
-    launch_decompress(compd, as<NielsD>(ws.pts), as<int>(ws.okflag), ns, st);
-    launch_niels_neg(as<NielsD>(ws.pts), as<NielsD>(ws.pts) + ns, ns, st);
-    int ok = 0;
-    BPG_HIP(hipMemcpyAsync(&ok, ws.okflag.p, 4, hipMemcpyDeviceToHost, st));
+    launch_decompress(compd, pts, ok_dev, ns, st);
+    BPG_HIP(hipMemcpyAsync(ok_host, ok_dev, 4, hipMemcpyDeviceToHost, st));
     ws.sync();
-    if (!ok) return 0;
     Scalar delta = from_dev(hsm[0]);
     Scalar wc = from_dev(wvh[m]);
+    vt.ns = ns;
+    vt.ss.assign(ns, Scalar::zero());
+    vt.ss[0] = x; vt.ss[1] = xx; vt.ss[2] = xxx;
+    for (uint32_t i = 0; i < m; i++) vt.ss[3 + i] = from_dev(wvh[i]) * rxx;
+    const Scalar Ts[5] = {r * x, rxx * x, rxx * xx, rxx * xxx, rxx * xx * xx};
+    for (int i = 0; i < 5; i++) vt.ss[3 + m + i] = Ts[i];
+    for (uint32_t k = 0; k < lgn; k++) { vt.ss[8 + m + k] = u2[k]; vt.ss[8 + m + lgn + k] = ui2[k]; }
+    vt.sB = w * (tx - pa * pb) + r * (xx * (wc + delta) - tx);
+    vt.sBb = -ebl - r * txb;
+    return 1;
+}
+
+// One shard of Verifier::verify's mega-check. Every shard replays the
+// transcript and the rejection checks; shard s of S sums the generator terms
+// j in [s N/S, (s+1) N/S) of G and H, shard 0 also the proof/commitment
+// points and the B, B_blinding terms. The shards' partial sums add up to the
+// point that must be the identity; `partial` (32 B, compressed) receives this
+// shard's part. Returns 1 (partial written, or accept when S == 1), 0 reject.
+int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                     const uint8_t *proof, size_t plen, const uint8_t entropy[32], uint32_t shard, uint32_t nshards,
+                     uint8_t *partial) {
+    if (nshards < 1 || shard >= nshards) throw std::runtime_error("bad shard");
+    DeviceContext &ctx = DeviceContext::get(cs.device);
+    const uint32_t N = cs.N;
+    if (plen < 1 || proof[0] != 0) return 0;
+    std::shared_ptr<const GenSet> gs = ctx.gens(N, 0, 1, true);
+    Workspace &ws = thread_workspace(cs.device);
+    hipStream_t st = ws.st;
+    ws.gh.grow((size_t)2 * N * sizeof(ScD) + 64);
+    const uint32_t ns_max = 3 + cs.m + 5 + 2 * 32;
+    ws.pts.grow(2 * (size_t)ns_max * sizeof(NielsD) + 64);   // points, then their negations
+    ws.okflag.grow(64);
+    int one = 1, ok = 0;
+    BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
+    VerifyTerms vt;
+    if (!verify_terms(cs, label, label_len, V, proof, plen, entropy, ws, as<ScD>(ws.gh), as<NielsD>(ws.pts),
+                      as<int>(ws.okflag), &ok, vt))
+        return 0;
+    if (!ok) return 0;
+    const uint32_t ns = vt.ns;
+    launch_niels_neg(as<NielsD>(ws.pts), as<NielsD>(ws.pts) + ns, ns, st);
+    ws.mscal.grow((size_t)ns * sizeof(ScD) + 64);
+    ScD *sscal = as<ScD>(ws.mscal);
     std::vector<ScD> ss(ns);
-    ss[0] = to_dev(x); ss[1] = to_dev(xx); ss[2] = to_dev(xxx);
-    for (uint32_t i = 0; i < m; i++) ss[3 + i] = to_dev(from_dev(wvh[i]) * rxx);
-    Scalar Ts[5] = {r * x, rxx * x, rxx * xx, rxx * xxx, rxx * xx * xx};
-    for (int i = 0; i < 5; i++) ss[3 + m + i] = to_dev(Ts[i]);
-    for (uint32_t k = 0; k < lgn; k++) { ss[8 + m + k] = to_dev(u2[k]); ss[8 + m + lgn + k] = to_dev(ui2[k]); }
+    for (uint32_t i = 0; i < ns; i++) ss[i] = to_dev(vt.ss[i]);
     BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)ns * sizeof(ScD), hipMemcpyHostToDevice, st));
     const uint64_t j0 = (uint64_t)N * shard / nshards, j1 = (uint64_t)N * (shard + 1) / nshards;
     const uint32_t cnt = (uint32_t)(j1 - j0);
@@ -1868,15 +1927,92 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
     Point R;
     combine_rows(R, ws.rows_host, pl.W, pl.c);
     if (shard == 0) {   // B and B_blinding terms
-        Scalar sB = w * (tx - pa * pb) + r * (xx * (wc + delta) - tx);
-        Scalar sBb = -ebl - r * txb;
         Point t1, t2;
-        mul_B(t1, sB); mul_B_blinding(t2, sBb);
+        mul_B(t1, vt.sB); mul_B_blinding(t2, vt.sBb);
         pt_add(R, R, t1); pt_add(R, R, t2);
     }
     if (nshards == 1) return pt_is_identity(R) ? 1 : 0;
     ristretto_compress(partial, R);
     return 1;
+}
+
+// Verifier::verify for `count` proofs of one circuit with one MSM (SURVEY
+// §8f "multi-proof batch verification"): proof j's verification equation
+// (a point that must be the identity) is weighted by a random scalar rho_j,
+// drawn from a transcript of every proof finalised with fresh entropy, and
+// the weighted sum is checked at once: its 2N generator terms carry
+// sum_j rho_j (g_j, h_j), accumulated on the device, and its small points
+// are all proofs' points. The identity means every proof is valid (but for
+// a ~1/l chance); otherwise, or when a proof fails a format check, each
+// remaining proof is verified alone. results[j] = 1 accept, 0 reject.
+void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                      const uint8_t *proofs, size_t stride, const size_t *lens, uint32_t count,
+                      const uint8_t entropy[32], int *results) {
+    if (!count) return;
+    DeviceContext &ctx = DeviceContext::get(cs.device);
+    const uint32_t N = cs.N;
+    std::shared_ptr<const GenSet> gs = ctx.gens(N, 0, 1, true);
+    Workspace &ws = thread_workspace(cs.device);
+    hipStream_t st = ws.st;
+    const uint32_t ns_max = 3 + cs.m + 5 + 2 * 32;
+    ws.gh.grow((size_t)2 * N * sizeof(ScD) + 64);
+    ws.ghacc.grow((size_t)2 * N * sizeof(ScD) + 64);
+    ws.pts.grow(2 * (size_t)count * ns_max * sizeof(NielsD) + 64);
+    ws.okflag.grow(64);
+    // the weights: bound to every proof and to entropy the prover cannot know
+    Transcript Tb((const uint8_t *)"bpg batch verify", 16);
+    Tb.append_message("label", label, label_len);
+    for (uint32_t j = 0; j < count; j++) Tb.append_message("proof", proofs + stride * (size_t)j, lens[j]);
+    TranscriptRng wr(Tb);
+    uint8_t ent[32];
+    thread_entropy().fill(ent, 32);
+    for (int i = 0; i < 32; i++) ent[i] ^= entropy[i];
+    wr.finalize(ent);
+    std::vector<Scalar> ss_all, rho(count);
+    std::vector<uint32_t> in_batch;
+    Scalar sB = Scalar::zero(), sBb = Scalar::zero();
+    uint32_t off = 0;
+    bool first = true;
+    for (uint32_t j = 0; j < count; j++) {
+        rho[j] = wr.random_scalar();
+        results[j] = 0;
+        int one = 1, ok = 0;
+        BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
+        VerifyTerms vt;
+        if (!verify_terms(cs, label, label_len, V, proofs + stride * (size_t)j, lens[j], entropy, ws,
+                          as<ScD>(ws.gh), as<NielsD>(ws.pts) + off, as<int>(ws.okflag), &ok, vt) || !ok)
+            continue;   // rejected on its own
+        launch_sc_axpy(as<ScD>(ws.ghacc), as<ScD>(ws.gh), 2 * N, mont(rho[j]), first, st);
+        first = false;
+        for (uint32_t i = 0; i < vt.ns; i++) ss_all.push_back(vt.ss[i] * rho[j]);
+        sB = sB + vt.sB * rho[j];
+        sBb = sBb + vt.sBb * rho[j];
+        off += vt.ns;
+        in_batch.push_back(j);
+    }
+    if (in_batch.empty()) return;
+    // one MSM: the weighted generator terms and every proof's small points
+    launch_niels_neg(as<NielsD>(ws.pts), as<NielsD>(ws.pts) + off, off, st);
+    ws.mscal.grow((size_t)off * sizeof(ScD) + 64);
+    ScD *sscal = as<ScD>(ws.mscal);
+    std::vector<ScD> ss(off);
+    for (uint32_t i = 0; i < off; i++) ss[i] = to_dev(ss_all[i]);
+    BPG_HIP(hipMemcpyAsync(sscal, ss.data(), (size_t)off * sizeof(ScD), hipMemcpyHostToDevice, st));
+    const int64_t gneg = gs->N;
+    MsmSeg seg[3] = {{as<ScD>(ws.ghacc), gs->G, N, 0, gneg}, {as<ScD>(ws.ghacc) + N, gs->H, N, 0, gneg},
+                     {sscal, ws.pts.p, off, 0, (int64_t)off}};
+    MsmPlan pl = ws.msm->enqueue(seg, 3, 1, ws.rows_host, MSM_NIELS);
+    ws.sync();
+    Point R, t1, t2;
+    combine_rows(R, ws.rows_host, pl.W, pl.c);
+    mul_B(t1, sB); mul_B_blinding(t2, sBb);
+    pt_add(R, R, t1); pt_add(R, R, t2);
+    if (pt_is_identity(R)) {
+        for (uint32_t j : in_batch) results[j] = 1;
+        return;
+    }
+    for (uint32_t j : in_batch)   // some proof is invalid: find which
+        results[j] = gpu_verify(cs, label, label_len, V, proofs + stride * (size_t)j, lens[j], entropy);
 }
 
 }  // namespace bpg

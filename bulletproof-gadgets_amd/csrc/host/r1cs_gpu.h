@@ -217,6 +217,7 @@ struct CommitPre {
     MsmPlan A, S[2];
     static const size_t ROWS_A = 0, ROWS_S0 = 256, ROWS_S1 = 384;
 };
+static const int MAX_LOCKSTEP = 4;   // proofs per lockstep step
 // The same for P (<= MAX_LOCKSTEP = 4) proofs of one circuit in lockstep on
 // the calling thread's stream (one MSM job per IPP step for all of them);
 // tms: P entries or null. P must be 1 when sharded. pre: P = 1 and the
@@ -225,9 +226,21 @@ struct CommitPre {
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms = nullptr,
                                                      const AllGather *ag = nullptr, const CommitPre *pre = nullptr);
+// The same for proofs of distinct prepared circuits of one shape (n, m, N):
+// proof p's circuit is csv[p] (distinct statements, bpg_prove_statements).
+std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *csv, const uint8_t *label,
+                                                     size_t label_len, const RngBlock *const *rbs, int P,
+                                                     ProveTimings *tms, const AllGather *ag = nullptr,
+                                                     const CommitPre *pre = nullptr);
 // Verifier::verify; returns 1 accept / 0 reject.
 int gpu_verify(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                const uint8_t *proof, size_t proof_len, const uint8_t entropy[32]);
+// Verifier::verify for `count` proofs of one circuit with one random-linear-
+// combination MSM (falls back to single verifications when the batch fails);
+// results[j] = 1 accept, 0 reject.
+void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                      const uint8_t *proofs, size_t stride, const size_t *lens, uint32_t count,
+                      const uint8_t entropy[32], int *results);
 // One shard of the verifier's mega-MSM (see r1cs_gpu.cpp); 1 = partial
 // written to `partial` (32 B), 0 = rejected by the shared checks.
 int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,

@@ -71,9 +71,11 @@ const char *bpg_last_error(void);
  * seeds == NULL: OS entropy), and out[k] receives what that c_prove returns
  * (release with free_proof), or NULL if statement k failed. `threads` CPU
  * workers synthesise and upload statements and draw the TranscriptRng
- * streams of up to 8 statements in lockstep; min(8, threads / 2) more
- * threads (bpg_set_statements_consumers overrides) drive the device, one HIP
- * stream each. Statements in flight are
+ * streams of up to 8 statements in lockstep; min(5, threads / 2) more
+ * threads (bpg_set_statements_layout overrides) drive the device, one HIP
+ * stream each, proving up to four ready statements of one shape (n, m, N)
+ * at once (their IPP MSM jobs merged, as in bpg_prove_batch). Statements in
+ * flight are
  * capped by HBM (free memory next to the device threads' workspaces, at the
  * footprint of the first prepared statement), and finished statements' device
  * arrays are recycled for the next ones. Returns the number of
@@ -84,9 +86,11 @@ int bpg_prove_statements(const char *name, const char *const *instances,
                          const uint64_t *seeds, uint32_t count, uint32_t threads,
                          struct ProofArtifacts **out);
 
-/* Added: device threads of later bpg_prove_statements calls of the process
- * (1-12; 0, the default: min(8, threads / 2)). -1 if out of range. */
-int bpg_set_statements_consumers(uint32_t consumers);
+/* Added: layout of later bpg_prove_statements calls of the process: device
+ * threads (1-12; 0, the default: min(5, threads / 2), fewer if HBM does not
+ * hold them) and statements each proves at once (1-4; 0, the default: 4).
+ * -1 if out of range. */
+int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep);
 
 /* Added: the last bpg_prove_statements of the process, per stage (ms summed
  * over threads; out[i], i < n <= 13): [0] CPU workers, [1] device consumers,

@@ -252,7 +252,8 @@ def test_batch_layouts_bit_exact(bpg, resources, producers, lockstep):
 
 
 def test_verify_batch(bpg, ctx, resources):
-    """bpg_verify_batch (config 5's batch verification): every valid proof of
+    """bpg_verify_batch (config 5's batch verification: chunks of proofs
+    checked by one random-linear-combination MSM each): every valid proof of
     a batch accepted, each tampered one rejected, same verdicts as the single
     verifier, whatever the thread count."""
     fx = read_fixture(os.path.join(resources, "or5"))
@@ -275,3 +276,12 @@ def test_verify_batch(bpg, ctx, resources):
     assert vprep.verify_batch(b"other label", V, proofs[:2], 2) == [False, False]
     with pytest.raises(bpg.BpgError):
         prep.verify_batch(b"vb", V, proofs[:1], 1)   # prover layout
+    # one chunk checked by a single random-linear-combination MSM: all valid
+    # -> accepted at once; one canonical-but-wrong proof inside -> the chunk
+    # fails and is re-verified proof by proof
+    many = prep.prove_batch(b"vb", [bytes([k + 40]) * 32 for k in range(20)], threads=2)
+    assert vprep.verify_batch(b"vb", V, many, 1) == [True] * 20
+    mixed = list(many)
+    b = bytearray(mixed[13]); b[300] ^= 4; mixed[13] = bytes(b)
+    assert vprep.verify_batch(b"vb", V, mixed, 1) == [k != 13 for k in range(20)]
+    assert vprep.verify_batch(b"vb", V, mixed, 3) == [k != 13 for k in range(20)]

@@ -115,6 +115,25 @@ def test_config5_batch_equals_single(bpg, ctx, W):
     assert len(set(batch)) == 3
 
 
+def test_config5_verify_batch(bpg, ctx, W):
+    """Batch verification at full size (2^20): eight proofs in one chunk are
+    accepted by one random-linear-combination MSM; with one of them tampered
+    (a canonical scalar changed, so only the final check can catch it) the
+    chunk falls back to single verifications and rejects exactly that one."""
+    inst, wit, gad = W.config5()
+    bpg.set_seed(57)
+    syn = bpg.Synth(inst, wit, gad)
+    prep = ctx.prepare(syn.view)
+    proofs = prep.prove_batch(b"vb5", [bytes([k + 9]) * 32 for k in range(8)], threads=4)
+    V = _V(ctx, syn)
+    vprep = ctx.prepare(syn.view, verifier=True)
+    assert vprep.verify_batch(b"vb5", V, proofs, 1) == [True] * 8
+    bad = bytearray(proofs[5])
+    bad[1 + 9 * 32 + 3] ^= 4            # t_x_blinding
+    mixed = proofs[:5] + [bytes(bad)] + proofs[6:]
+    assert vprep.verify_batch(b"vb5", V, mixed, 1) == [k != 5 for k in range(8)]
+
+
 def test_config5_batch_hbm_admission(bpg, W):
     """HBM-aware admission: another allocation in the
     process holds all but 64 GB of the free HBM and the layout asks for 28

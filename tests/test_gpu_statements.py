@@ -2,8 +2,10 @@
 once): statement k must give exactly the bytes of
 `set_seed(seeds[k]); c_prove(name, *statement_k)` — the same synthesis,
 commitments and proof — although its TranscriptRng stream is drawn in
-lockstep with up to 7 other statements of different sizes, and a statement
-that fails to synthesise yields None without disturbing the others."""
+lockstep with up to 7 other statements of different sizes, distinct
+statements of one shape are proved up to four at a time in lockstep (their
+IPP MSM jobs merged), and a statement that fails to synthesise yields None
+without disturbing the others."""
 import os
 
 import pytest
@@ -52,3 +54,18 @@ def test_prove_statements_matches_c_prove(bpg):
     assert st["limit"] <= 4 * 6 + 8 + 2 * 3
     assert st["bound_stage"] in ("cpu workers (synthesis + prepare + rng)", "device consumers")
     assert st["synth_ms"] > 0 and st["prove_ms"] > 0 and st["rng_ms"] > 0
+
+
+def test_prove_statements_same_shape_lockstep(bpg):
+    """Distinct statements of one shape (config 2 with different seeds: other
+    witnesses, Merkle roots and set elements, the same n, m, N) are proved in
+    lockstep by the device threads; each proof still equals its own c_prove."""
+    import workloads as W
+    sts = [W.config2(3100 + k) for k in range(9)]
+    seeds = [900 + k for k in range(len(sts))]
+    out = bpg.prove_statements("same", sts, threads=4, seeds=seeds)
+    for k, (st, seed) in enumerate(zip(sts, seeds)):
+        bpg.set_seed(seed)
+        want = bpg.prove("same", *st)
+        assert out[k] == want, k
+    assert len(set(o[0] for o in out)) == len(sts)
