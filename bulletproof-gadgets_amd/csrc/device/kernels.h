@@ -44,6 +44,12 @@ void set_prof_sink(ProfSink *s);   // thread-local
 // ~100% CPU), and with a 16-core CPU share the spinning threads got the whole
 // process throttled while the GPU idled.
 void event_wait(hipEvent_t ev);
+// Set once the process has begun to exit (an atexit handler registered with
+// the first device context): the destructors of process-lifetime device
+// objects then leave their memory to the OS instead of calling into a HIP
+// runtime that may already be tearing down.
+bool process_exiting();
+void mark_process_exiting();
 ProfSink *prof_sink();
 
 // -------------------------------------------------------------- points

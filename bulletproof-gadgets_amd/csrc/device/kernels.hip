@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "dev_field.h"
@@ -70,6 +71,9 @@ static constexpr int BPG_COMB_PRIO = 0;
 
 static thread_local ProfSink *tl_sink = nullptr;
 void set_prof_sink(ProfSink *s) { tl_sink = s; }
+static std::atomic<bool> g_exiting(false);
+bool process_exiting() { return g_exiting.load(); }
+void mark_process_exiting() { g_exiting = true; }
 void event_wait(hipEvent_t ev) {
     const long spin_us = 50;
     for (;;) {
@@ -917,6 +921,7 @@ static int msm_window(uint64_t total, int nmsm, int fmt) {
 }
 
 MsmEngine::~MsmEngine() {
+    if (process_exiting()) return;
     if (tiles_ev_) (void)hipEventDestroy(tiles_ev_);
     if (tiles_host_) (void)hipHostFree(tiles_host_);
     DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_,

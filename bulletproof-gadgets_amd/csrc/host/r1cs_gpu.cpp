@@ -37,6 +37,11 @@ DeviceContext &DeviceContext::get(int device) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     auto &p = ctxs[device];
     if (!p) {
+        static bool hooked = false;
+        if (!hooked) {   // runs before `ctxs` and the later statics are destroyed
+            hooked = true;
+            std::atexit(dev::mark_process_exiting);
+        }
         p.reset(new DeviceContext());
         p->device = device;
         BPG_HIP(hipSetDevice(device));
@@ -64,16 +69,19 @@ DeviceContext &DeviceContext::get(int device) {
 }
 
 GenSet::~GenSet() {
+    if (dev::process_exiting()) return;
     if (G || H) (void)hipSetDevice(device);
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
 }
 FbTables::~FbTables() {
+    if (dev::process_exiting()) return;
     if (G || H) (void)hipSetDevice(device);
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
 }
 CombTables::~CombTables() {
+    if (dev::process_exiting()) return;
     if (tabG || tabH) (void)hipSetDevice(device);
     if (tabG) (void)hipFree(tabG);
     if (tabH) (void)hipFree(tabH);
@@ -372,6 +380,7 @@ struct Workspace : dev::ProfSink {
         event_wait(done_ev);
     }
     ~Workspace() {
+        if (dev::process_exiting()) return;
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (done_ev) (void)hipEventDestroy(done_ev);
         if (rows_host) (void)hipHostFree(rows_host);
@@ -772,6 +781,7 @@ ProducerStage &producer_stage(int device) {
     return *p;
 }
 ProducerStage::~ProducerStage() {
+    if (dev::process_exiting()) return;
     for (int b = 0; b < 2; b++) {
         if (host[b]) (void)hipHostFree(host[b]);
         if (ev[b]) (void)hipEventDestroy(ev[b]);
