@@ -1535,15 +1535,10 @@ void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundA
     BPG_HIP(hipGetLastError());
 }
 // u, uinv in Montgomery form
-struct FoldScalarsArgs { sc *a[4], *b[4]; sc um[4], uim[4]; };
-// a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u for the P proofs of a
-// lockstep step (blockIdx.y = proof): one launch per round, not one per proof
-__global__ void k_ipp_fold_scalars(FoldScalarsArgs A, uint32_t h) {
+__global__ void k_ipp_fold_scalars(sc *__restrict__ a, sc *__restrict__ b, uint32_t h, sc um, sc uim) {
     WAVE_PRIO(BPG_MISC_PRIO);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= h) return;
-    sc *a = A.a[p], *b = A.b[p];
-    const sc um = A.um[p], uim = A.uim[p];
     sc x, y, t1, t2;
     sc_load(x, a + i); sc_load(y, a + h + i); mm(t1, x, um); mm(t2, y, uim); sc_add(t1, t1, t2); sc_store(a + i, t1);
     sc_load(x, b + i); sc_load(y, b + h + i); mm(t1, x, uim); mm(t2, y, um); sc_add(t1, t1, t2); sc_store(b + i, t1);
@@ -1567,15 +1562,9 @@ void launch_sc_axpy(ScD *acc, const ScD *x, uint32_t count, ScD rho_mont, bool f
                        *reinterpret_cast<sc *>(&rho_mont), first ? 1 : 0);
     BPG_HIP(hipGetLastError());
 }
-void launch_ipp_fold_scalars(ScD *const *a, ScD *const *b, const ScD *u, const ScD *uinv, int P, uint32_t h,
-                             hipStream_t st) {
-    if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "fold scalars proofs", __FILE__, __LINE__);
-    FoldScalarsArgs A{};
-    for (int p = 0; p < P; p++) {
-        A.a[p] = AS_SC(a[p]); A.b[p] = AS_SC(b[p]);
-        A.um[p] = *reinterpret_cast<const sc *>(&u[p]); A.uim[p] = *reinterpret_cast<const sc *>(&uinv[p]);
-    }
-    hipLaunchKernelGGL(k_ipp_fold_scalars, dim3(nblk(h, 256), P), dim3(256), 0, st, A, h);
+void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st) {
+    hipLaunchKernelGGL(k_ipp_fold_scalars, dim3(nblk(h, 256)), dim3(256), 0, st, AS_SC(a), AS_SC(b), h,
+                       *reinterpret_cast<sc *>(&u), *reinterpret_cast<sc *>(&uinv));
     BPG_HIP(hipGetLastError());
 }
 // Point fold: out_i = P_L,i + rho * P_R,i with one rho per lane class. rho is
@@ -2492,29 +2481,24 @@ void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppR
     hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
-struct TailWeightArgs { sc *wG[4], *wH[4]; sc r[4][4]; };   // per proof: rGa, rGb, rHa, rHb
-__global__ void k_ipp_tail_weights(TailWeightArgs A, uint32_t M, uint32_t h, uint32_t n) {
+__global__ void k_ipp_tail_weights(sc *__restrict__ wG, sc *__restrict__ wH, uint32_t M, uint32_t h, uint32_t n,
+                                   sc rGa, sc rGb, sc rHa, sc rHb) {
     WAVE_PRIO(BPG_MISC_PRIO);
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= M) return;
     const uint32_t i = j % (2 * h);
     if (i < h) return;
     const uint32_t il = i - h;
     const bool bcls = il < n && il + h >= n;
-    sc *wG = A.wG[p], *wH = A.wH[p];
     sc w;
-    sc_load(w, wG + j); mm(w, w, A.r[p][bcls ? 1 : 0]); sc_store(wG + j, w);
-    sc_load(w, wH + j); mm(w, w, A.r[p][bcls ? 3 : 2]); sc_store(wH + j, w);
+    sc_load(w, wG + j); mm(w, w, bcls ? rGb : rGa); sc_store(wG + j, w);
+    sc_load(w, wH + j); mm(w, w, bcls ? rHb : rHa); sc_store(wH + j, w);
 }
-void launch_ipp_tail_weights(ScD *const *wG, ScD *const *wH, const ScD (*r)[4], int P, uint32_t M, uint32_t h,
-                             uint32_t n, hipStream_t st) {
-    if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "tail weights proofs", __FILE__, __LINE__);
-    TailWeightArgs A{};
-    for (int p = 0; p < P; p++) {
-        A.wG[p] = AS_SC(wG[p]); A.wH[p] = AS_SC(wH[p]);
-        for (int k = 0; k < 4; k++) A.r[p][k] = *reinterpret_cast<const sc *>(&r[p][k]);
-    }
-    hipLaunchKernelGGL(k_ipp_tail_weights, dim3(nblk(M, 256), P), dim3(256), 0, st, A, M, h, n);
+void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t n, ScD rGa, ScD rGb, ScD rHa,
+                             ScD rHb, hipStream_t st) {
+    hipLaunchKernelGGL(k_ipp_tail_weights, dim3(nblk(M, 256)), dim3(256), 0, st, AS_SC(wG), AS_SC(wH), M, h, n,
+                       *reinterpret_cast<sc *>(&rGa), *reinterpret_cast<sc *>(&rGb), *reinterpret_cast<sc *>(&rHa),
+                       *reinterpret_cast<sc *>(&rHb));
     BPG_HIP(hipGetLastError());
 }
 

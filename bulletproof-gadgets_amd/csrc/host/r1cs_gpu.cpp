@@ -1470,7 +1470,6 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
         ws.prof_end(ph);
         ws.sync();
         std::vector<std::array<Scalar, 4>> rnow(P);   // this round's fold scalars (G a/b, H a/b)
-        ScD *fa[MAX_LOCKSTEP], *fb[MAX_LOCKSTEP], fu[MAX_LOCKSTEP], fui[MAX_LOCKSTEP];   // a, b folds
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             Point LR[2], cq;
@@ -1492,24 +1491,19 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             T[p].append_point("R", cr);
             const Scalar uk = T[p].challenge_scalar("u");
             const Scalar uinv = sc_invert(uk);
-            fa[p] = as<ScD>(B.a); fb[p] = as<ScD>(B.b); fu[p] = mont(uk); fui[p] = mont(uinv);
+            launch_ipp_fold_scalars(as<ScD>(B.a), as<ScD>(B.b), h, mont(uk), mont(uinv), st);
             const Scalar u2 = uk * uk, ui2 = uinv * uinv;
             const Scalar yh = sc_pow_u64(y_inv[p], (uint64_t)h * world);   // the round's global half length
             rnow[p] = {u2, u2 * u[p], ui2 * yh, ui2 * yh * u[p]};
             lam[p] = lam[p] * uinv;
             mu[p] = mu[p] * uk;
         }
-        launch_ipp_fold_scalars(fa, fb, fu, fui, P, h, st);   // the round's a, b folds of every proof
         const int nxt = cur == 0 ? 1 : 0;
         if (tail) {
-            if (h > 1 || sharded) {
-                ScD *wg[MAX_LOCKSTEP], *wh[MAX_LOCKSTEP], rw[MAX_LOCKSTEP][4];
-                for (int p = 0; p < P; p++) {
-                    wg[p] = as<ScD>(ws.pb[p].wG); wh[p] = as<ScD>(ws.pb[p].wH);
-                    for (int q = 0; q < 4; q++) rw[p][q] = mont(rnow[p][q]);
-                }
-                launch_ipp_tail_weights(wg, wh, rw, P, M, h, nl, st);
-            }
+            if (h > 1 || sharded)
+                for (int p = 0; p < P; p++)
+                    launch_ipp_tail_weights(as<ScD>(ws.pb[p].wG), as<ScD>(ws.pb[p].wH), M, h, nl, mont(rnow[p][0]),
+                                            mont(rnow[p][1]), mont(rnow[p][2]), mont(rnow[p][3]), st);
         } else if (h > 1) {
             const int group = (comb && cur < 0) ? 2 : group_cfg;
             if (depth + 1 < group) {   // level k + depth + 1 stays implicit

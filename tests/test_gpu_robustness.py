@@ -27,6 +27,17 @@ def bpg():
     return workloads._bpg()
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _room_for_workers(bpg):
+    """The workers are fresh processes on the same GPU: this process first
+    hands back what earlier tests left cached (comb tables, generator slices,
+    the thread pool's workspaces; bpg_ctx_trim), so a worker does not start
+    with most of the HBM held by its parent (round 4 saw a worker that had
+    printed its results exit on SIGSEGV under that pressure)."""
+    bpg.Context(0).trim()
+    yield
+
+
 def run(*args):
     r = subprocess.run([sys.executable, WORKER] + list(args), capture_output=True, text=True, timeout=200)
     assert r.returncode == 0, r.stderr[-3000:]
