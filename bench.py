@@ -86,8 +86,11 @@ def parse():
     return ap.parse_args()
 
 
-# single kernels bracketed live (bpg name -> rocprofv3 kernel name)
-KERNELS = {"msm_pass1_niels": "k_rbk_pass<true, 1, true>", "msm_pass1_cached": "k_rbk_pass<true, 0, false>",
+# single kernels bracketed live (bpg name -> rocprofv3 kernel name); every
+# label brackets exactly one kernel instantiation, so a label's launch count,
+# average and bytes are that rocprof kernel's
+KERNELS = {"msm_pass1_gens": "k_rbk_pass<true, 1, true>", "msm_pass1_folded": "k_rbk_pass<true, 1, false>",
+           "msm_pass1_cached": "k_rbk_pass<true, 0, false>",
            "ipp_fold_points": "k_ipp_fold_points<gec>",
            "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "ipp_fold3": "k_ipp_fold3<gec>",
            "flatten": "k_flatten_short"}
@@ -474,6 +477,11 @@ def main():
         achieved = (by / lc) / sec / 1e9         # GB/s of algorithmic bytes
         pmc = pmc_row(KERNELS[dom])
         prof = prof_row(KERNELS[dom])
+        # traffic: the PMC passes' HBM bytes per launch of the same kernel
+        # (FETCH_SIZE x 2 + WRITE_SIZE, separate passes); the PMC run's own
+        # algorithmic bytes per launch of that kernel (same label, same
+        # job mix) give the over-fetch ratio
+        pmc_alg = pmc.get("alg_bytes_per_launch")
         roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm",
                 # the HBM fraction is the metric's; the kernel is limited by its
                 # GF(p) multiply rate and gather latency, see "valu"
@@ -481,6 +489,10 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": pmc.get("hbm_bytes_per_launch"), "launches": lc, "avg_launch_ms": round(sec * 1e3, 4),
                 "alg_bytes_per_launch": round(by / lc, 1),
+                "traffic_source": {"pmc_alg_bytes_per_launch": pmc_alg,
+                                   "traffic_over_alg": round(pmc["hbm_bytes_per_launch"] / pmc_alg, 2)
+                                   if pmc_alg and pmc.get("hbm_bytes_per_launch") else None,
+                                   "pmc_source": pmc.get("source")} if pmc else None,
                 # the kernels are VALU-bound (255-bit field arithmetic): the same
                 # launches against the measured GF(p) multiply peak
                 "valu": {"unit": "G fe_mul/s", "achieved": round(fm / lc / sec / 1e9, 2), "peak": FEMUL_PEAK_G,
@@ -497,6 +509,13 @@ def main():
                 "rocprof_default_cmd": dict(prof, frac=round((by / lc) / (prof["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 6))
                 if prof else None,
                 "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
+                # every bracketed kernel: launches, average launch and
+                # algorithmic bytes per launch (scripts/pmc_table.py reads this
+                # table from its own run to pair the PMC bytes with them)
+                "kernel_table": {k: {"rocprof_name": KERNELS[k], "launches": v[0],
+                                     "avg_launch_ms": round(v[1] / v[0], 4),
+                                     "alg_bytes_per_launch": round(v[2] / v[0], 1)}
+                                 for k, v in kernels.items()},
                 "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items() if v}}
 
     total_proofs = a.steps * batch * world

@@ -393,10 +393,11 @@ class Context:
             raise BpgError("bad pipeline layout")
 
     def setup_stats(self):
-        arr = (ctypes.c_double * 6)()
-        lib().bpg_ctx_setup_stats(self.h, arr, 6)
+        arr = (ctypes.c_double * 10)()
+        lib().bpg_ctx_setup_stats(self.h, arr, 10)
         return {"gens_ms": arr[0], "comb_ms": arr[1], "gens_from_cache": bool(arr[2]), "comb_alloc_ms": arr[3],
-                "comb_bytes": arr[4], "msm_table_bytes": arr[5]}
+                "comb_bytes": arr[4], "msm_table_bytes": arr[5], "workspaces_parked": int(arr[6]),
+                "workspace_parks": int(arr[7]), "stages_parked": int(arr[8]), "stage_parks": int(arr[9])}
 
     def trim(self):
         """bpg_ctx_trim: drop cached comb tables / generator slices no proof

@@ -1157,8 +1157,16 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     p.passes = 0;
     for (;;) {
         const uint32_t nblocks = (uint32_t)std::max<uint64_t>(1, (E + RBK_CHUNK - 1) / RBK_CHUNK);
-        // pass 1 consumes the job's operands: 64-B point + 32-B scalar each (SURVEY §8d)
-        ProfScope ps(p.passes ? nullptr : (fmt == MSM_CACHED ? "msm_pass1_cached" : "msm_pass1_niels"),
+        // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
+        // (SURVEY §8d). One label per kernel instantiation, so a label's
+        // launches are exactly one rocprof kernel: generator jobs (Niels bases
+        // with pre-negated copies, k_rbk_pass<true, 1, true>), folded IPP
+        // levels (Niels, negated in registers, <true, 1, false>) and cached
+        // bases (<true, 0, false>).
+        ProfScope ps(p.passes ? nullptr
+                              : (fmt == MSM_CACHED ? "msm_pass1_cached"
+                                 : negc            ? "msm_pass1_gens"
+                                                   : "msm_pass1_folded"),
                      96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels;
                      // each lane's first entry is a 1M conversion
                      (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0 -

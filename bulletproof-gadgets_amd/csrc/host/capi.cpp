@@ -186,8 +186,11 @@ int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n) {
     double resident = 0, fb = 0;
     for (auto &e : c.combs) resident += (double)e.second->bytes;
     for (auto &e : c.fbs) fb += (double)e.second->bytes;
-    const double v[6] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms, resident, fb};
-    for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
+    const ParkStats ps = park_stats();
+    const double v[10] = {c.gens_ms, c.comb_ms, c.gens_from_cache ? 1.0 : 0.0, c.comb_alloc_ms, resident, fb,
+                          (double)ps.workspaces_parked, (double)ps.workspace_parks, (double)ps.stages_parked,
+                          (double)ps.stage_parks};
+    for (int i = 0; i < n && i < 10; i++) out[i] = v[i];
     return 0;
 }
 int bpg_gens_ensure(bpg_ctx *ctx, uint32_t capacity) {
@@ -415,8 +418,10 @@ int64_t bpg_ctx_trim(bpg_ctx *ctx) {
         const int dev = ctx->device;
         std::atomic<int64_t> ws(0);
         const int nw = pool().size();
-        if (nw) pool().run(nw, [&](int) { ws += (int64_t)release_thread_workspace(dev); });
+        // (and the producer stages' pinned host buffers, which are not counted)
+        if (nw) pool().run(nw, [&](int) { ws += (int64_t)release_thread_workspace(dev); release_producer_stage(dev); });
         ws += (int64_t)release_thread_workspace(dev);
+        release_producer_stage(dev);
         {
             std::lock_guard<std::mutex> lk(g_held_mu);
             g_held.erase(dev);

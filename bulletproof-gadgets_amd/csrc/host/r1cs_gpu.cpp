@@ -5,8 +5,11 @@
 // and src/r1cs/proof.rs `to_bytes` / `from_bytes`.
 #include "r1cs_gpu.h"
 
+#include <execinfo.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <stdlib.h>
+#include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -31,6 +34,37 @@ static double now_ms() {
 }
 
 // ------------------------------------------------------------------ context
+// Fatal-signal report: a native backtrace on stderr before the default
+// action (the round-4 exit-time SIGSEGV left no stack). Installed with the
+// first device context, only for signals nobody else handles (an embedding
+// runtime's own handler, e.g. Python's faulthandler, is left alone).
+static void crash_report(int sig) {
+    char msg[64] = "bpg: fatal signal ";
+    size_t k = strlen(msg);
+    if (sig >= 10) msg[k++] = (char)('0' + sig / 10);
+    msg[k++] = (char)('0' + sig % 10);
+    memcpy(msg + k, ", native backtrace:\n", 21);
+    (void)!write(2, msg, strlen(msg));
+    void *bt[64];
+    const int n = backtrace(bt, 64);
+    backtrace_symbols_fd(bt, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+static void install_crash_report() {
+    void *warm[2];
+    (void)backtrace(warm, 2);   // loads the unwinder now, not inside the handler
+    for (int sig : {SIGSEGV, SIGBUS, SIGILL, SIGFPE}) {
+        struct sigaction cur;
+        if (sigaction(sig, nullptr, &cur) != 0 || (cur.sa_flags & SA_SIGINFO) || cur.sa_handler != SIG_DFL) continue;
+        struct sigaction sa;
+        memset(&sa, 0, sizeof(sa));
+        sa.sa_handler = crash_report;
+        sigemptyset(&sa.sa_mask);
+        sa.sa_flags = SA_RESETHAND | SA_NODEFER;
+        sigaction(sig, &sa, nullptr);
+    }
+}
 static std::mutex g_ctx_mu;
 DeviceContext &DeviceContext::get(int device) {
     static std::map<int, std::unique_ptr<DeviceContext>> ctxs;
@@ -41,6 +75,7 @@ DeviceContext &DeviceContext::get(int device) {
         if (!hooked) {   // runs before `ctxs` and the later statics are destroyed
             hooked = true;
             std::atexit(dev::mark_process_exiting);
+            install_crash_report();
         }
         p.reset(new DeviceContext());
         p->device = device;
@@ -440,15 +475,94 @@ struct Workspace : dev::ProfSink {
     }
 };
 
-static std::map<int, std::unique_ptr<Workspace>> &thread_workspaces() {
-    static thread_local std::map<int, std::unique_ptr<Workspace>> wss;
-    return wss;
+// Thread-owned device resources (workspaces, producer stages) and thread exit.
+// A thread's exit never frees them: it parks them in a process-wide list
+// (heap-allocated and never destroyed), and the next thread that needs one
+// for the device takes it over. Freeing happens only in explicit calls
+// (bpg_ctx_trim) while the process is live.
+//
+// Why (round-4 SIGSEGV, profiles/r04u_gpu_tests_exit_segv.log): a Python
+// thread's join() returns when its interpreter state is released, BEFORE the
+// OS thread runs its C++ thread_local destructors. The robustness worker
+// joined its two proving threads, printed its results and exited while those
+// threads were still in ~Workspace (hipFree of GBs, hipHostFree,
+// hipStreamDestroy): glibc's exit() ran the HIP runtime's teardown
+// concurrently with them, and the process died with SIGSEGV after its
+// output. The exiting flag did not help: it is set by an atexit handler,
+// i.e. after the race has begun (and the exiting thread's own TLS
+// destructors run before atexit handlers anyway). With nothing done in
+// thread exit but a list insertion under a mutex there is no race left.
+template <class T>
+struct Parked {
+    std::mutex mu;
+    std::multimap<int, T *> items;   // device -> resource
+    uint64_t parked_total = 0;       // thread exits that parked one (diagnostics)
+    void put(int device, T *t) {
+        std::lock_guard<std::mutex> lk(mu);
+        items.emplace(device, t);
+        parked_total++;
+    }
+    T *take(int device) {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = items.find(device);
+        if (it == items.end()) return nullptr;
+        T *t = it->second;
+        items.erase(it);
+        return t;
+    }
+    std::vector<T *> take_all(int device) {
+        std::lock_guard<std::mutex> lk(mu);
+        std::vector<T *> out;
+        auto r = items.equal_range(device);
+        for (auto it = r.first; it != r.second; ++it) out.push_back(it->second);
+        items.erase(r.first, r.second);
+        return out;
+    }
+};
+template <class T>
+static Parked<T> &parked() {
+    static Parked<T> *p = new Parked<T>();   // never destroyed: outlives every thread
+    return *p;
+}
+template <class T>
+struct ThreadOwned {   // one thread's resources by device; parked on thread exit
+    std::map<int, T *> m;
+    ~ThreadOwned() {
+        for (auto &e : m)
+            if (e.second) parked<T>().put(e.first, e.second);
+    }
+};
+static std::map<int, Workspace *> &thread_workspaces() {
+    static thread_local ThreadOwned<Workspace> wss;
+    return wss.m;
+}
+ParkStats park_stats() {
+    ParkStats s;
+    {
+        Parked<Workspace> &p = parked<Workspace>();
+        std::lock_guard<std::mutex> lk(p.mu);
+        s.workspaces_parked = p.items.size();
+        s.workspace_parks = p.parked_total;
+    }
+    {
+        Parked<ProducerStage> &p = parked<ProducerStage>();
+        std::lock_guard<std::mutex> lk(p.mu);
+        s.stages_parked = p.items.size();
+        s.stage_parks = p.parked_total;
+    }
+    return s;
 }
 Workspace &thread_workspace(int device) {
     auto &p = thread_workspaces()[device];
+    if (!p && (p = parked<Workspace>().take(device))) {   // a finished thread's workspace
+        BPG_HIP(hipSetDevice(device));
+        BPG_HIP(hipStreamSynchronize(p->st));
+        p->pend.clear();   // timing brackets its last owner never flushed
+        p->ev_next = 0;
+    }
     if (!p) {
         BPG_HIP(hipSetDevice(device));
-        p.reset(new Workspace());
+        p = new Workspace();
         p->device = device;
         BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
         BPG_HIP(hipEventCreateWithFlags(&p->done_ev, hipEventBlockingSync | hipEventDisableTiming));
@@ -457,26 +571,38 @@ Workspace &thread_workspace(int device) {
         BPG_HIP(hipHostGetDevicePointer((void **)&p->rows_view, p->rows_host, 0));
         BPG_HIP(hipHostMalloc((void **)&p->small_host, 4096 * sizeof(ScD), hipHostMallocDefault));
     }
-    dev::set_prof_sink(p.get());   // this thread's launches record on its own stream
+    dev::set_prof_sink(p);   // this thread's launches record on its own stream
     BPG_HIP(hipSetDevice(device));
     return *p;
 }
+static size_t workspace_bytes(const Workspace &ws);
 size_t release_thread_workspace(int device) {
     auto &m = thread_workspaces();
     auto it = m.find(device);
-    if (it == m.end() || !it->second) return 0;
-    const size_t b = thread_workspace_bytes(device);
+    size_t b = 0;
     BPG_HIP(hipSetDevice(device));
-    BPG_HIP(hipStreamSynchronize(it->second->st));
-    dev::set_prof_sink(nullptr);
-    m.erase(it);
+    if (it != m.end() && it->second) {
+        b += workspace_bytes(*it->second);
+        BPG_HIP(hipStreamSynchronize(it->second->st));
+        dev::set_prof_sink(nullptr);
+        delete it->second;
+    }
+    if (it != m.end()) m.erase(it);
+    // and the workspaces finished threads left behind
+    for (Workspace *w : parked<Workspace>().take_all(device)) {
+        b += workspace_bytes(*w);
+        BPG_HIP(hipStreamSynchronize(w->st));
+        delete w;
+    }
     return b;
 }
 size_t thread_workspace_bytes(int device) {
     auto &m = thread_workspaces();
     auto it = m.find(device);
     if (it == m.end() || !it->second) return 0;
-    const Workspace &ws = *it->second;
+    return workspace_bytes(*it->second);
+}
+static size_t workspace_bytes(const Workspace &ws) {
     size_t b = ws.msm ? ws.msm->bytes() : 0;
     for (const DBuf *d : {&ws.w, &ws.yipm, &ws.zlo, &ws.zhi, &ws.ylo, &ws.yhi, &ws.tabs, &ws.mscal, &ws.partial,
                           &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag, &ws.ghacc, &ws.vcomp})
@@ -763,12 +889,36 @@ static Transcript prover_transcript(const PreparedCS &cs, const uint8_t *label, 
 // all) go to one stream per producer thread: one stream shared by all
 // producers (fewer streams than hardware queues for the consumers) measured
 // 62.3 / 62.4 vs 70.8 / 69.7 M constraints/s (profiles/r03a_ab_producer_streams.txt).
+static std::map<int, ProducerStage *> &thread_stages() {
+    static thread_local ThreadOwned<ProducerStage> m;   // parked on thread exit (see Parked)
+    return m.m;
+}
+size_t release_producer_stage(int device) {
+    auto &m = thread_stages();
+    std::vector<ProducerStage *> all = parked<ProducerStage>().take_all(device);
+    auto it = m.find(device);
+    if (it != m.end()) {
+        if (it->second) all.push_back(it->second);
+        m.erase(it);
+    }
+    size_t b = 0;
+    BPG_HIP(hipSetDevice(device));
+    for (ProducerStage *s : all) {
+        BPG_HIP(hipStreamSynchronize(s->st));
+        b += 2 * (size_t)8 * ProducerStage::CHUNK * 64 + s->one_cap;
+        delete s;
+    }
+    return b;
+}
 ProducerStage &producer_stage(int device) {
-    static thread_local std::map<int, std::unique_ptr<ProducerStage>> m;
-    auto &p = m[device];
+    auto &p = thread_stages()[device];
+    if (!p && (p = parked<ProducerStage>().take(device))) {
+        BPG_HIP(hipSetDevice(device));
+        BPG_HIP(hipStreamSynchronize(p->st));
+    }
     if (!p) {
         BPG_HIP(hipSetDevice(device));
-        p.reset(new ProducerStage());
+        p = new ProducerStage();
         BPG_HIP(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
         for (int b = 0; b < 2; b++) {
             BPG_HIP(hipHostMalloc((void **)&p->host[b], (size_t)8 * ProducerStage::CHUNK * 64, hipHostMallocDefault));

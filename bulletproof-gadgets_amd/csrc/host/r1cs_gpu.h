@@ -150,8 +150,12 @@ struct Workspace;
 Workspace &thread_workspace(int device);
 // Device bytes held by the calling thread's workspace on `device` (0: none).
 size_t thread_workspace_bytes(int device);
-// Free the calling thread's workspace on `device` (bpg_ctx_trim); its bytes.
+// Free the calling thread's workspace on `device` and those finished threads
+// parked (bpg_ctx_trim); their bytes. A thread's exit frees nothing: it parks
+// its workspaces / producer stages for the next thread (r1cs_gpu.cpp Parked).
 size_t release_thread_workspace(int device);
+struct ParkStats { uint64_t workspaces_parked = 0, workspace_parks = 0, stages_parked = 0, stage_parks = 0; };
+ParkStats park_stats();
 // HBM admission estimates: what a workspace proving P proofs of `cs` in
 // lockstep grows to, and what one Verifier::verify of a circuit of its size
 // needs on a fresh workspace.
@@ -185,6 +189,9 @@ struct ProducerStage {
     ~ProducerStage();
 };
 ProducerStage &producer_stage(int device);
+// Free the calling thread's producer stage on `device` and the parked ones
+// (bpg_ctx_trim); their pinned bytes.
+size_t release_producer_stage(int device);
 // Draw the RNG streams of `count` (<= 8) proofs of `cs` in lockstep. With
 // dev_out the s_L | s_R draws go to out[k]->wide as device buffers, and
 // `progress(v, ev)` (if given, dev_out only) is called once all s_L (v = 0)

@@ -216,13 +216,18 @@ int bpg_ctx_set_ipp_tail(bpg_ctx *ctx, int lanes);
  * (or loading) generators, out[1] ms building comb tables, out[2] 1 if the
  * generators came from the on-disk cache, out[3] ms of out[1] spent
  * allocating the tables' memory, out[4] bytes of comb tables resident,
- * out[5] bytes of fixed-base MSM tables resident (n <= 6). */
+ * out[5] bytes of fixed-base MSM tables resident, out[6] / out[7] device
+ * workspaces parked now / parked in all by exiting threads, out[8] / out[9]
+ * the same for producer stages (n <= 10). A thread that proved and exits
+ * frees nothing (no HIP call runs in a thread's exit, where it could race
+ * the process's own teardown): its workspace waits for the next thread. */
 int bpg_ctx_setup_stats(bpg_ctx *ctx, double *out, int n);
 /* Release the device's cached comb tables and sharded generator slices that
  * no proof in flight holds, and the batch worker pool's (and the caller's)
- * per-thread device workspaces (they are rebuilt on next use): lets another
- * process or circuit size on the same GPU have the HBM. Call it between
- * batches. Returns the bytes released, < 0 on error. */
+ * per-thread device workspaces and those exited threads parked (they are
+ * rebuilt on next use): lets another process or circuit size on the same GPU
+ * have the HBM. Call it between batches. Returns the bytes released, < 0 on
+ * error. */
 int64_t bpg_ctx_trim(bpg_ctx *ctx);
 
 /* Ensure G_i, H_i for i < capacity are resident (BulletproofGens::new(cap,1),

@@ -20,6 +20,16 @@ fetch, write, sq, grbm = J(0, "counter_collection"), J(1, "counter_collection"),
     J(3, "counter_collection")
 trace = J(2, "kernel_trace")
 SIMDS = 1024
+# the bench line the FETCH_SIZE pass printed: its live per-label table gives
+# the algorithmic bytes per launch of each bracketed kernel in THIS run (same
+# job mix as the counters), so hbm / alg is the kernel's over-fetch ratio
+alg = {}
+try:
+    line = [ln for ln in open("%s_pmc0.json" % pre) if ln.startswith("{")][-1]
+    for lab, r in ((json.loads(line).get("roofline") or {}).get("kernel_table") or {}).items():
+        alg[r["rocprof_name"]] = dict(r, label=lab)
+except (OSError, IndexError, ValueError):
+    pass
 rows = {}
 for k, c in sq.items():
     t = trace.get(k, {})
@@ -41,14 +51,20 @@ for k, c in sq.items():
         "wave_wait_issue": c.get("SQ_WAIT_INST_ANY", 0) / wc,
         "valu_insts_per_wave": c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_WAVES", 1), 1),
     }
+    if k in alg:
+        a = alg[k]["alg_bytes_per_launch"]
+        rows[k].update(label=alg[k]["label"], alg_bytes_per_launch=a, bench_launches=alg[k]["launches"],
+                       hbm_over_alg=hbm / a if a else None)
 order = sorted(rows, key=lambda k: -rows[k]["avg_us"] * rows[k]["dispatches"])
-print("| kernel | launches | avg us | GHz | HBM B/launch | HBM GB/s | VALU issue share | waves/SIMD | "
-      "wave active | wait mem | wait issue |")
-print("|---|---|---|---|---|---|---|---|---|---|---|")
+print("| kernel | launches | avg us | GHz | HBM B/launch | alg B/launch | HBM/alg | HBM GB/s | VALU issue share | "
+      "waves/SIMD | wave active | wait mem | wait issue |")
+print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
 for k in order[:24]:
     r = rows[k]
-    print("| %s | %d | %.1f | %.2f | %.3g | %.0f | %.3f | %.2f | %.2f | %.2f | %.2f |" % (
-        k, r["dispatches"], r["avg_us"], r["clock_ghz"], r["hbm_bytes_per_launch"], r["hbm_gbs"] or 0,
+    print("| %s | %d | %.1f | %.2f | %.3g | %s | %s | %.0f | %.3f | %.2f | %.2f | %.2f | %.2f |" % (
+        k, r["dispatches"], r["avg_us"], r["clock_ghz"], r["hbm_bytes_per_launch"],
+        "%.3g" % r["alg_bytes_per_launch"] if r.get("alg_bytes_per_launch") else "",
+        "%.1f" % r["hbm_over_alg"] if r.get("hbm_over_alg") else "", r["hbm_gbs"] or 0,
         r["valu_issue_share"] or 0, r["avg_waves_per_simd"] or 0, r["wave_active"], r["wave_wait_mem"],
         r["wave_wait_issue"]))
 if len(sys.argv) > 2:

@@ -1,5 +1,5 @@
 """Child process of tests/test_gpu_robustness.py (a fresh device context per
-run). usage: robust_worker.py cache <dir> | concurrent"""
+run). usage: robust_worker.py cache <dir> | concurrent | exit"""
 import json
 import os
 import sys
@@ -44,8 +44,43 @@ def main():
             t.start()
         for t in ts:
             t.join()
-        print(json.dumps(out))
+        # no wait here: the process exits while the OS threads may still be
+        # running their thread-exit code (the round-4 SIGSEGV's window)
+        print(json.dumps(dict(out, park=bpg.Context(0).setup_stats())), flush=True)
+
+
+def exit_with_live_workspaces():
+    """The low-HBM path (no comb tables) on three threads, and an exit with
+    device workspaces still owned: the main thread's (its thread_local
+    destructors run inside exit()), one finished thread's, and one thread
+    still alive (blocked) when the process exits."""
+    import workloads as W
+    bpg = W._bpg()
+    bpg.set_seed(3)
+    syn = bpg.Synth(*W.config3())
+    ctx = bpg.Context(0)
+    ctx.set_strategy(fold_tables=0)
+    hold = threading.Event()
+    out = {}
+
+    def prove(k, block):
+        out[k] = ctx.r1cs_prove(b"exit", syn.view, bytes([len(k)]) * 32)[0].hex()
+        if block:
+            hold.wait()   # never set: alive at exit
+    done = threading.Thread(target=prove, args=("done", False))
+    live = threading.Thread(target=prove, args=("live", True), daemon=True)
+    done.start()
+    live.start()
+    prove("main", False)
+    done.join()
+    while "live" not in out:
+        hold.wait(0.05)
+    print(json.dumps(dict(out, park=ctx.setup_stats())), flush=True)
 
 
 if __name__ == "__main__":
+    if sys.argv[1] == "exit":
+        sys.path[:0] = [ROOT]
+        exit_with_live_workspaces()
+        sys.exit(0)
     main()

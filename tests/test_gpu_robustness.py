@@ -7,8 +7,15 @@
 * two circuit sizes proved concurrently from two host threads on a fresh
   context (the larger circuit grows the generator set while the smaller
   circuit's proofs hold their snapshot) give the same bytes as sequential
-  proving.
+  proving;
+* thread exit and process exit (round 4's SIGSEGV, DESIGN.md "Thread exit"):
+  a worker exits right after joining its proving threads, and one exits with
+  device workspaces still owned by its main thread and by a live thread, on
+  the low-HBM path (no comb tables) -- both with this process still holding
+  what earlier tests left cached (no trim first); a thread's exit parks its
+  workspace, the next thread takes it over.
 """
+import threading
 import json
 import os
 import subprocess
@@ -27,20 +34,10 @@ def bpg():
     return workloads._bpg()
 
 
-@pytest.fixture(scope="module", autouse=True)
-def _room_for_workers(bpg):
-    """The workers are fresh processes on the same GPU: this process first
-    hands back what earlier tests left cached (comb tables, generator slices,
-    the thread pool's workspaces; bpg_ctx_trim), so a worker does not start
-    with most of the HBM held by its parent (round 4 saw a worker that had
-    printed its results exit on SIGSEGV under that pressure)."""
-    bpg.Context(0).trim()
-    yield
-
-
 def run(*args):
     r = subprocess.run([sys.executable, WORKER] + list(args), capture_output=True, text=True, timeout=200)
     assert r.returncode == 0, r.stderr[-3000:]
+    assert "bpg: fatal signal" not in r.stderr, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
@@ -73,3 +70,36 @@ def test_concurrent_circuit_sizes(bpg):
         syn = bpg.Synth(*stmt)
         want = [ctx.r1cs_prove(b"conc", syn.view, bytes([r]) * 32)[0].hex() for r in range(reps)]
         assert conc[k] == want, k
+
+
+def test_exit_with_live_workspaces():
+    out = run("exit")
+    assert all(len(out[k]) > 800 for k in ("main", "done", "live"))
+
+
+def test_thread_exit_parks_workspace(bpg):
+    """A proving thread's exit hands its device workspace to the next thread
+    (no HIP call in thread exit); bpg_ctx_trim frees the parked ones."""
+    import time
+    import workloads as W
+    ctx = bpg.Context(0)
+    syn = bpg.Synth(*W.config2())
+
+    def prove_on_new_thread():
+        res = []
+        t = threading.Thread(target=lambda: res.append(ctx.r1cs_prove(b"park", syn.view, bytes(32))[0]))
+        t.start()
+        t.join()
+        return res[0]
+
+    s0 = ctx.setup_stats()
+    a = prove_on_new_thread()
+    deadline = time.time() + 10   # the OS thread finishes its exit after join()
+    while ctx.setup_stats()["workspace_parks"] == s0["workspace_parks"] and time.time() < deadline:
+        time.sleep(0.01)
+    s1 = ctx.setup_stats()
+    assert s1["workspace_parks"] == s0["workspace_parks"] + 1 and s1["workspaces_parked"] >= 1
+    b = prove_on_new_thread()     # takes the parked workspace over
+    assert a == b
+    assert ctx.trim() >= 0
+    assert ctx.setup_stats()["workspaces_parked"] == 0
