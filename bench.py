@@ -91,8 +91,10 @@ def parse():
 # average and bytes are that rocprof kernel's
 KERNELS = {"msm_pass1_gens": "k_rbk_pass<true, 1, true>", "msm_pass1_folded": "k_rbk_pass<true, 1, false>",
            "msm_pass1_cached": "k_rbk_pass<true, 0, false>",
-           "ipp_fold_points": "k_ipp_fold_points<gec>",
-           "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "ipp_fold3": "k_ipp_fold3<gec>",
+           "ipp_fold_points": "k_ipp_fold_points<gec>", "ipp_fold_points_niels": "k_ipp_fold_points<gen>",
+           "ipp_fold2_niels": "k_ipp_fold2<gen, 3>",
+           "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "ipp_fold3": "k_ipp_fold3<gen>",
+           "ipp_fold3_cached": "k_ipp_fold3<gec>",
            "flatten": "k_flatten_short"}
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 FEMUL_PEAK_G = 261.5         # GF(2^255-19) multiplies/s x1e9, measured: profiles/r02d_valu_micro.log (fe_variants V2)
@@ -580,6 +582,7 @@ def pipeline_line(p, ncpu, per_rank, pinned, nproofs):
             if p["producer_draw_ms"] else None,
             "proofs_per_s": round(nproofs / (p["wall_ms"] / 1e3), 2),
             "consumers_by_threads": p["consumers_by_threads"], "consumers_by_hbm": p["consumers_by_hbm"],
+            "hw_queues": p["hw_queues"],
             "est_gb_per_consumer": round(p["est_gb_per_consumer"], 2), "hbm_free_gb_at_start": round(p["hbm_free_gb"], 1),
             "cpus": {"job": ncpu, "rank_share": per_rank, "process": p["process_cpus"], "pinned": pinned or None}}
 

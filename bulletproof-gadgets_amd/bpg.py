@@ -581,7 +581,7 @@ def last_timings():
 
 BATCH_STATS = ("producers", "consumers", "lockstep", "inflight", "wall_ms", "fill_ms", "consumer_starved_ms",
                "producer_slot_wait_ms", "producer_draw_ms", "consumer_prove_ms", "host_bound", "hbm_free_gb",
-               "est_gb_per_consumer", "consumers_by_threads", "consumers_by_hbm", "process_cpus")
+               "est_gb_per_consumer", "consumers_by_threads", "consumers_by_hbm", "process_cpus", "hw_queues")
 
 
 def last_batch_stats():
@@ -591,7 +591,7 @@ def last_batch_stats():
     d = dict(zip(BATCH_STATS, arr))
     d["host_bound"] = bool(d["host_bound"])
     for k in ("producers", "consumers", "lockstep", "inflight", "consumers_by_threads", "consumers_by_hbm",
-              "process_cpus"):
+              "process_cpus", "hw_queues"):
         d[k] = int(d[k])
     return d
 

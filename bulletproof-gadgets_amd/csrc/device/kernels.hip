@@ -281,10 +281,14 @@ struct TileGeo {
 __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G, uint32_t wstride) {
     WAVE_PRIO(BPG_SORT_PRIO);
-    __shared__ uint32_t gofs[MSM_MAXSEG + 1];
+    // the segment table in LDS: a per-lane (runtime) index into the kernel
+    // argument struct would copy it to scratch
+    __shared__ uint32_t gofs[MSM_MAXSEG + 1], srow0[MSM_MAXSEG];
+    __shared__ const sc *sscal[MSM_MAXSEG];
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     if (threadIdx.x <= (uint32_t)T.n) gofs[threadIdx.x] = T.gofs[threadIdx.x];
+    if (threadIdx.x < (uint32_t)T.n) { srow0[threadIdx.x] = T.row0[threadIdx.x]; sscal[threadIdx.x] = T.scal[threadIdx.x]; }
     __syncthreads();
     for (uint64_t q = g; q < G.bflag_bytes / 16; q += stride) reinterpret_cast<uint4 *>(G.bflag)[q] = uint4{0, 0, 0, 0};
     if (G.tiles) {
@@ -311,15 +315,21 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
     if (g >= total) return;
     int si = seg_of(gofs, T.n, g);
     sc k;
-    sc_load(k, T.scal[si] + (g - T.gofs[si]));
+    sc_load(k, sscal[si] + (g - gofs[si]));
     uint32_t carry = 0, mask = (1u << c) - 1, full = 1u << c;
-    const uint32_t m = T.row0[si];
-    const uint32_t loc = (uint32_t)si << MSM_SEG_SHIFT | (g - T.gofs[si]);
+    const uint32_t m = srow0[si];
+    const uint32_t loc = (uint32_t)si << MSM_SEG_SHIFT | (g - gofs[si]);
     for (int w = 0; w < W; w++) {
         int bit = w * c;
         int lo = bit >> 5, sh = bit & 31;
-        uint64_t x = k.v[lo];
-        if (lo + 1 < 8) x |= (uint64_t)k.v[lo + 1] << 32;
+        // words lo and lo + 1 by selects (no runtime index into k.v: scratch)
+        uint32_t x0 = 0, x1 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            x0 = lo == j ? k.v[j] : x0;
+            x1 = lo + 1 == j ? k.v[j] : x1;
+        }
+        const uint64_t x = (uint64_t)x0 | (uint64_t)x1 << 32;
         uint32_t d = (uint32_t)(x >> sh) & mask;
         d += carry;
         // rows window-major (row = w nmsm + m), or one per MSM for a
@@ -1368,6 +1378,8 @@ template <int K>
 DEVI void block_reduce_store(sc (&v)[K], sc *__restrict__ partial) {
     __shared__ sc sh[256];
     uint32_t tid = threadIdx.x;
+    // unrolled: v[] stays in registers (a runtime index put it in scratch)
+#pragma unroll
     for (int k = 0; k < K; k++) {
         sc_store(&sh[tid], v[k]);
         for (int s = 128; s >= 1; s >>= 1) {
@@ -1741,7 +1753,7 @@ void launch_ipp_fold_points(const void *Gin, const void *Hin, int in_fmt, uint32
         for (uint32_t d = 1; d < S.ndig; d++) dbl += S.gap[d];
         fem += (double)(A.end[k] - A.start[k]) * (7.0 * dbl + 8.0 * S.ndig + 40.0);
     }
-    ProfScope ps("ipp_fold_points", 6.0 * h * 64, fem);
+    ProfScope ps(in_fmt == MSM_NIELS ? "ipp_fold_points_niels" : "ipp_fold_points", 6.0 * h * 64, fem);
     if (in_fmt == MSM_NIELS)
         hipLaunchKernelGGL(k_ipp_fold_points<gen>, dim3(blocks), dim3(64), 0, st, reinterpret_cast<const FoldArgs *>(stage.dev));
     else
@@ -1943,7 +1955,7 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(Fold2Args), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
     // reads 4 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
-    ProfScope ps("ipp_fold2", 2.0 * h1 * 5 * 64, fem);
+    ProfScope ps(in_fmt == MSM_NIELS ? "ipp_fold2_niels" : "ipp_fold2", 2.0 * h1 * 5 * 64, fem);
     const Fold2Args *dA = reinterpret_cast<const Fold2Args *>(stage.dev);
     if (in_fmt == MSM_NIELS) hipLaunchKernelGGL((k_ipp_fold2<gen, WN>), dim3(blocks), dim3(64), 0, st, dA);
     else hipLaunchKernelGGL((k_ipp_fold2<gec, WN>), dim3(blocks), dim3(64), 0, st, dA);
@@ -2154,7 +2166,7 @@ void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq,
     BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldNArgs), hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
     // reads 8 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
-    ProfScope ps("ipp_fold3", 2.0 * hq * 9 * 64, fem);
+    ProfScope ps(in_fmt == MSM_NIELS ? "ipp_fold3" : "ipp_fold3_cached", 2.0 * hq * 9 * 64, fem);   // one label per kernel
     const FoldNArgs *dA = reinterpret_cast<const FoldNArgs *>(stage.dev);
     if (in_fmt == MSM_NIELS) hipLaunchKernelGGL(k_ipp_fold3<gen>, dim3(blocks), dim3(64), 0, st, dA);
     else hipLaunchKernelGGL(k_ipp_fold3<gec>, dim3(blocks), dim3(64), 0, st, dA);

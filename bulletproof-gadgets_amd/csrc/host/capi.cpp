@@ -447,6 +447,20 @@ static uint32_t process_cpus() {
     }
     return n;
 }
+// Hardware queues HIP gives this process: GPU_MAX_HW_QUEUES as the runtime
+// read it when it initialised (its default, 4, when unset). Each consumer
+// thread drives its own HIP stream; streams beyond the queues share them in
+// order and serialise behind each other's kernels (47.0 vs 51.9 M
+// constraints/s with 8 streams on 4 queues, profiles/r01h_sweep.txt), so
+// the batch layouts size their device streams to this.
+static uint32_t hw_queues() {
+    static const uint32_t q = [] {
+        const char *e = getenv("GPU_MAX_HW_QUEUES");
+        const long v = e ? atol(e) : 0;
+        return (uint32_t)(v > 0 ? v : 4);
+    }();
+    return q;
+}
 static double since_ms(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
@@ -488,6 +502,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
         if (P >= threads && threads > 1) P = threads - 1;
         const uint32_t C_req = std::max<uint32_t>(1, threads > P ? threads - P : 1);
         uint32_t C = std::min<uint32_t>(C_req, (count + L - 1) / L);
+        C = std::min<uint32_t>(C, hw_queues());   // one hardware queue per consumer stream
         // proofs in flight: at most max_inflight (default 24 at N = 2^20,
         // scaled by 1/N: a proof in flight holds ~3.1 GB next to the 208 GB
         // of comb tables, profiles/r03u_bench.json hbm_used_gb), and what
@@ -650,7 +665,8 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
             const double v[BPG_BATCH_STATS] = {(double)P, (double)C, (double)L, (double)(C * L), wall, fill_ms,
                                                starve_ms, slot_wait_ms, draw_ms, prove_ms,
                                                starve_ms / span > 0.10 ? 1.0 : 0.0, free_b / 1e9, est_c / 1e9,
-                                               (double)C_req, (double)C_hbm, (double)process_cpus()};
+                                               (double)C_req, (double)C_hbm, (double)process_cpus(),
+                                               (double)hw_queues()};
             memcpy(g_bs, v, sizeof(v));
         }
         if (!err.empty()) throw std::runtime_error(err);
@@ -703,7 +719,8 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         // bpg_prove_batch does for one circuit)
         const uint32_t l_set = g_stmt_lockstep.load();
         const uint32_t L = l_set ? l_set : 4;
-        const uint32_t C = std::min<uint32_t>(c_set ? 12 : 5, std::max<uint32_t>(1, c_set ? c_set : W / 2));
+        const uint32_t C = std::min<uint32_t>(std::min<uint32_t>(c_set ? 12 : 5, hw_queues()),
+                                              std::max<uint32_t>(1, c_set ? c_set : W / 2));
         const size_t label_len = strlen(name);
         const uint8_t *label = (const uint8_t *)name;
         struct Item {

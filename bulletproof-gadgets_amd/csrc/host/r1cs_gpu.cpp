@@ -403,13 +403,14 @@ struct Workspace : dev::ProfSink {
     int device = 0;
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
-    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag, ghacc, vcomp;
+    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag, ghacc, vcomp, ones;
     PtD *rows_host = nullptr;        // pinned, 2 x ROWS_HALF window rows
     PtD *rows_view = nullptr;        // its device view (the row kernels write there)
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
     size_t s_host_cap = 0;
     ScD *small_host = nullptr;       // pinned small transfers (4096 scalars)
     hipEvent_t done_ev = nullptr;    // blocking-sync event: waiting threads sleep instead of spinning
+    hipEvent_t stage_wiped = nullptr;   // s_host zeroed after its last proof
     void sync() {
         BPG_HIP(hipEventRecord(done_ev, st));
         event_wait(done_ev);
@@ -418,11 +419,12 @@ struct Workspace : dev::ProfSink {
         if (dev::process_exiting()) return;
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (done_ev) (void)hipEventDestroy(done_ev);
+        if (stage_wiped) (void)hipEventDestroy(stage_wiped);
         if (rows_host) (void)hipHostFree(rows_host);
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&w, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs, &mscal, &partial, &small, &gh, &ynwR, &pts, &okflag,
-                        &ghacc, &vcomp};
+                        &ghacc, &vcomp, &ones};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -605,7 +607,7 @@ size_t thread_workspace_bytes(int device) {
 static size_t workspace_bytes(const Workspace &ws) {
     size_t b = ws.msm ? ws.msm->bytes() : 0;
     for (const DBuf *d : {&ws.w, &ws.yipm, &ws.zlo, &ws.zhi, &ws.ylo, &ws.yhi, &ws.tabs, &ws.mscal, &ws.partial,
-                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag, &ws.ghacc, &ws.vcomp})
+                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag, &ws.ghacc, &ws.vcomp, &ws.ones})
         b += d->cap;
     for (const ProofBufs &B : ws.pb)
         for (const DBuf *d : {&B.wide, &B.sL, &B.sR, &B.w, &B.wloc, &B.l1, &B.r0, &B.r1, &B.r3, &B.ypm, &B.yipm,
@@ -664,7 +666,11 @@ std::vector<uint8_t *> PreparedCS::slots(size_t count, size_t bytes, bool host) 
 
 PreparedCS::~PreparedCS() {
     for (uint8_t *b : slot_bufs) (void)hipFree(b);
-    for (uint8_t *b : host_slot_bufs) (void)hipHostFree(b);
+    // pinned RNG slots held raw blinding draws: zeroed before they go back
+    for (uint8_t *b : host_slot_bufs) {
+        memset(b, 0, host_slot_bytes);
+        (void)hipHostFree(b);
+    }
     DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols};
     for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
 }
@@ -926,6 +932,8 @@ ProducerStage &producer_stage(int device) {
             BPG_HIP(hipEventRecord(p->ev[b], p->st));
             BPG_HIP(hipEventCreateWithFlags(&p->drawn[b], hipEventDisableTiming));
         }
+        BPG_HIP(hipEventCreateWithFlags(&p->wiped, hipEventBlockingSync | hipEventDisableTiming));
+        BPG_HIP(hipEventRecord(p->wiped, p->st));
     }
     BPG_HIP(hipSetDevice(device));
     return *p;
@@ -937,6 +945,7 @@ ProducerStage::~ProducerStage() {
         if (ev[b]) (void)hipEventDestroy(ev[b]);
         if (drawn[b]) (void)hipEventDestroy(drawn[b]);
     }
+    if (wiped) (void)hipEventDestroy(wiped);
     if (one) (void)hipHostFree(one);
     if (st) (void)hipStreamDestroy(st);
 }
@@ -988,7 +997,11 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         ProducerStage &ps = producer_stage(cs.device);
         const uint64_t BIG = 32768;
         uint8_t *h = out[0]->stage;
-        if (!h) {
+        const bool own = !h;
+        if (own) {
+            // the previous proof's copies out of this buffer, and its wipe,
+            // are complete
+            BPG_HIP(hipEventSynchronize(ps.wiped));
             if (ps.one_cap < 64 * nd) {
                 if (ps.one) BPG_HIP(hipHostFree(ps.one));
                 ps.one = nullptr;
@@ -996,8 +1009,6 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
                 ps.one_cap = 64 * nd;
             }
             h = ps.one;
-            // the previous proof's copies out of this buffer are complete
-            BPG_HIP(hipEventSynchronize(ps.drawn[1]));
         }
         for (int v = 0; v < 2; v++) {
             const uint64_t a = v ? nd / 2 : 0, b = v ? nd : nd / 2;
@@ -1015,6 +1026,10 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         if (!progress) {
             BPG_HIP(hipEventRecord(ps.drawn[1], ps.st));
             event_wait(ps.drawn[1]);
+        }
+        if (own) {   // behind the copies on the same stream (no draws left in pinned memory)
+            BPG_HIP(hipMemsetAsync(h, 0, (size_t)64 * nd, ps.st));
+            BPG_HIP(hipEventRecord(ps.wiped, ps.st));
         }
     } else {
         // stream chunks of draws through two pinned staging buffers into
@@ -1048,6 +1063,12 @@ void rng_draw_group(const PreparedCS &cs, const uint8_t *label, size_t label_len
         }
         event_wait(ps.ev[0]);
         event_wait(ps.ev[1]);
+        // the staging buffers' last chunks are blinding draws: zeroed behind
+        // their copies; the next group's first chunk waits on ev[] as before
+        for (int b = 0; b < 2; b++) {
+            BPG_HIP(hipMemsetAsync(ps.host[b], 0, (size_t)8 * CH * 64, ps.st));
+            BPG_HIP(hipEventRecord(ps.ev[b], ps.st));
+        }
     }
     for (int j = 0; j < 5; j++) {
         draw(tp);
@@ -1163,6 +1184,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         pre.S[v] = ws.msm->enqueue(&seg, 1, 1, rows + off, MSM_NIELS, rows_dev + off);
         ws.prof_end(ph);
     };
+    if (ws.stage_wiped) BPG_HIP(hipEventSynchronize(ws.stage_wiped));   // the last proof's wipe of s_host
     ws.stage(2 * (size_t)n * 64 + 64);
     RngBlock rb;
     rb.wide = as<uint8_t>(B.wide);
@@ -1174,6 +1196,11 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     ProveTimings t;
     const RngBlock *crb = &rb;
     std::vector<uint8_t> pr = gpu_prove_lockstep(cs, label, label_len, &crb, 1, &t, ag, &pre)[0];
+    // s_host holds this proof's s_L / s_R draws: zeroed on the stream that
+    // read them, waited for by the next proof before it draws
+    if (!ws.stage_wiped) BPG_HIP(hipEventCreateWithFlags(&ws.stage_wiped, hipEventBlockingSync | hipEventDisableTiming));
+    BPG_HIP(hipMemsetAsync(ws.s_host, 0, 2 * (size_t)n * 64, ws.st));
+    BPG_HIP(hipEventRecord(ws.stage_wiped, ws.st));
     t.rng_ms = t1 - t0;
     t.total_ms += t1 - t0;
     last_timings() = t;
@@ -1225,6 +1252,31 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // batch, or distinct statements of one shape (n, m, N: the IPP and every
 // MSM job depend only on those; a_L/a_R/a_O, the constraint matrix and the
 // commitments are each proof's own).
+// sum_{j in [a, b)} H_j of a generator set (one MSM with unit scalars on the
+// workspace's stream, once per range; rows land in the commitment half of the
+// pinned row buffer, which is free once the commitments are combined).
+static Point generator_range_sum(Workspace &ws, const GenSet &gs, uint32_t a, uint32_t b) {
+    {
+        std::lock_guard<std::mutex> lk(gs.sums_mu);
+        auto it = gs.h_sums.find({a, b});
+        if (it != gs.h_sums.end()) return it->second;
+    }
+    Point S;
+    pt_identity(S);
+    if (b > a) {
+        const uint32_t cnt = b - a;
+        ws.ones.grow((size_t)cnt * sizeof(ScD) + 64);
+        launch_fill_scalars(as<ScD>(ws.ones), to_dev(Scalar::one()), cnt, ws.st);
+        const MsmSeg seg = {as<ScD>(ws.ones), gs.H + a, cnt, 0, (int64_t)gs.N};
+        MsmPlan pl = ws.msm->enqueue(&seg, 1, 1, ws.rows_host, MSM_NIELS);
+        ws.sync();
+        combine_rows(S, ws.rows_host, pl.W, pl.c);
+    }
+    std::lock_guard<std::mutex> lk(gs.sums_mu);
+    gs.h_sums[{a, b}] = S;
+    return S;
+}
+
 std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                                      const RngBlock *const *rbs, int P, ProveTimings *tms,
                                                      const AllGather *ag, const CommitPre *pre) {
@@ -1551,6 +1603,12 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
         auto at = [&](const void *b, size_t i) { return (const void *)((const uint8_t *)b + i * ps); };
         const bool lazy = depth == 1;
         const size_t hh = h;
+        // round 0 over the level-0 generators with padding lanes: their L
+        // terms on H_lo become one precomputed sum (below)
+        const bool round0_pad = k == 0 && cur < 0 && depth == 0 && !tail && nl > h && nl < len;
+        Point pad_sum;
+        if (round0_pad)   // before the job: the sum's MSM uses the workspace's engine and row buffer
+            pad_sum = generator_range_sum(ws, *gs, nl - h, h);
         MsmSeg seg[MSM_MAX_SEGS];
         int nseg = 0;
         for (int p = 0; p < P; p++) {
@@ -1606,9 +1664,15 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             } else {
                 launch_ipp_prep(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, ms, as<ScD>(B.partial), cout, st);
                 // points whose a-scalar is zero (padding lanes) are left out of
-                // the job: L's G part runs over a_lo, R's over a_hi
+                // the job: L's G part runs over a_lo, R's over a_hi. In round
+                // 0 L's H part leaves out the padding lanes too: there
+                // b_hi[j] * y^-j = -y^(j + h) y^-j = -y^h for every padding
+                // lane (r(x) is -y^i past the real lanes, prover.rs pads it so),
+                // so their terms are -y^h * sum H_j over a fixed range, added
+                // on the host (pad_sum): 29% of round 0's L entries at 2^20
                 const uint32_t nLG = std::min(h, anz), nRG = anz > h ? std::min(h, anz - h) : 0u;
-                const MsmSeg sl[4] = {{ms, at(Gm, h), nLG, L0, gn}, {ms + hh, Hm, h, L0, gn},
+                const uint32_t nLH = round0_pad ? nl - h : h;
+                const MsmSeg sl[4] = {{ms, at(Gm, h), nLG, L0, gn}, {ms + hh, Hm, nLH, L0, gn},
                                       {ms + 2 * hh, Gm, nRG, R0, gn}, {ms + 3 * hh, at(Hm, h), h, R0, gn}};
                 for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
             }
@@ -1625,6 +1689,12 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             Point LR[2], cq;
             combine_rows(LR[0], rowsLR + (2 * p) * pl.W, pl.W, pl.c);
             combine_rows(LR[1], rowsLR + (2 * p + 1) * pl.W, pl.W, pl.c);
+            if (round0_pad) {   // the padding lanes' L terms: -y^(h world) mu * sum H_j
+                const Scalar spad = -(sc_pow_u64(y[p], (uint64_t)h * world) * mu[p]);
+                Point t;
+                mul_var(t, spad, pad_sum);
+                pt_add(LR[0], LR[0], t);
+            }
             // + c_L Q, + c_R Q (this rank's share of c_L, c_R when sharded)
             for (int s = 0; s < 2; s++) {
                 mul_B(cq, from_dev(B.small_host[1020 + s]) * wch[p]);
@@ -2097,18 +2167,27 @@ int gpu_verify_shard(const PreparedCS &cs, const uint8_t *label, size_t label_le
 // the weighted sum is checked at once: its 2N generator terms carry
 // sum_j rho_j (g_j, h_j), accumulated on the device, and its small points
 // are all proofs' points. The identity means every proof is valid (but for
-// a ~1/l chance); otherwise, or when a proof fails a format check, each
-// remaining proof is verified alone. results[j] = 1 accept, 0 reject.
-void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
-                      const uint8_t *proofs, size_t stride, const size_t *lens, uint32_t count,
-                      const uint8_t entropy[32], int *results) {
-    if (!count) return;
+// a ~1/l chance). Otherwise the set is split in halves, each checked the same
+// way with fresh weights, down to pairs verified alone: one invalid proof in
+// a chunk of 64 costs 1 + 2 lg 64 = 13 MSMs instead of 65 (a
+// single bad proof must not buy 64 extra 2N-point MSMs). results[j] = 1
+// accept, 0 reject.
+static void verify_batch_set(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                             const uint8_t *proofs, size_t stride, const size_t *lens,
+                             const std::vector<uint32_t> &idx, const uint8_t entropy[32], int *results) {
+    if (idx.empty()) return;
+    if (idx.size() <= 2) {
+        for (uint32_t j : idx)
+            results[j] = gpu_verify(cs, label, label_len, V, proofs + stride * (size_t)j, lens[j], entropy);
+        return;
+    }
     DeviceContext &ctx = DeviceContext::get(cs.device);
     const uint32_t N = cs.N;
     std::shared_ptr<const GenSet> gs = ctx.gens(N, 0, 1, true);
     Workspace &ws = thread_workspace(cs.device);
     hipStream_t st = ws.st;
     const uint32_t ns_max = 3 + cs.m + 5 + 2 * 32;
+    const uint32_t count = (uint32_t)idx.size();
     ws.gh.grow((size_t)2 * N * sizeof(ScD) + 64);
     ws.ghacc.grow((size_t)2 * N * sizeof(ScD) + 64);
     ws.pts.grow(2 * (size_t)count * ns_max * sizeof(NielsD) + 64);
@@ -2116,19 +2195,19 @@ void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_l
     // the weights: bound to every proof and to entropy the prover cannot know
     Transcript Tb((const uint8_t *)"bpg batch verify", 16);
     Tb.append_message("label", label, label_len);
-    for (uint32_t j = 0; j < count; j++) Tb.append_message("proof", proofs + stride * (size_t)j, lens[j]);
+    for (uint32_t j : idx) Tb.append_message("proof", proofs + stride * (size_t)j, lens[j]);
     TranscriptRng wr(Tb);
     uint8_t ent[32];
     thread_entropy().fill(ent, 32);
     for (int i = 0; i < 32; i++) ent[i] ^= entropy[i];
     wr.finalize(ent);
-    std::vector<Scalar> ss_all, rho(count);
+    std::vector<Scalar> ss_all;
     std::vector<uint32_t> in_batch;
     Scalar sB = Scalar::zero(), sBb = Scalar::zero();
     uint32_t off = 0;
     bool first = true;
-    for (uint32_t j = 0; j < count; j++) {
-        rho[j] = wr.random_scalar();
+    for (uint32_t j : idx) {
+        const Scalar rho = wr.random_scalar();
         results[j] = 0;
         int one = 1, ok = 0;
         BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
@@ -2136,11 +2215,11 @@ void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_l
         if (!verify_terms(cs, label, label_len, V, proofs + stride * (size_t)j, lens[j], entropy, ws,
                           as<ScD>(ws.gh), as<NielsD>(ws.pts) + off, as<int>(ws.okflag), &ok, vt) || !ok)
             continue;   // rejected on its own
-        launch_sc_axpy(as<ScD>(ws.ghacc), as<ScD>(ws.gh), 2 * N, mont(rho[j]), first, st);
+        launch_sc_axpy(as<ScD>(ws.ghacc), as<ScD>(ws.gh), 2 * N, mont(rho), first, st);
         first = false;
-        for (uint32_t i = 0; i < vt.ns; i++) ss_all.push_back(vt.ss[i] * rho[j]);
-        sB = sB + vt.sB * rho[j];
-        sBb = sBb + vt.sBb * rho[j];
+        for (uint32_t i = 0; i < vt.ns; i++) ss_all.push_back(vt.ss[i] * rho);
+        sB = sB + vt.sB * rho;
+        sBb = sBb + vt.sBb * rho;
         off += vt.ns;
         in_batch.push_back(j);
     }
@@ -2165,8 +2244,22 @@ void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_l
         for (uint32_t j : in_batch) results[j] = 1;
         return;
     }
-    for (uint32_t j : in_batch)   // some proof is invalid: find which
-        results[j] = gpu_verify(cs, label, label_len, V, proofs + stride * (size_t)j, lens[j], entropy);
+    // some proof is invalid: bisect, fresh weights per half
+    const size_t h = in_batch.size() / 2;
+    verify_batch_set(cs, label, label_len, V, proofs, stride, lens,
+                     std::vector<uint32_t>(in_batch.begin(), in_batch.begin() + h), entropy, results);
+    verify_batch_set(cs, label, label_len, V, proofs, stride, lens,
+                     std::vector<uint32_t>(in_batch.begin() + h, in_batch.end()), entropy, results);
+}
+void gpu_verify_batch(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
+                      const uint8_t *proofs, size_t stride, const size_t *lens, uint32_t count,
+                      const uint8_t entropy[32], int *results) {
+    std::vector<uint32_t> idx;
+    for (uint32_t j = 0; j < count; j++) {
+        results[j] = 0;
+        if (lens[j] <= stride) idx.push_back(j);   // a longer "proof" would read past its slot: rejected
+    }
+    verify_batch_set(cs, label, label_len, V, proofs, stride, lens, idx, entropy, results);
 }
 
 }  // namespace bpg

@@ -36,6 +36,10 @@ struct GenSet {
     // G, H: N points each, followed in the same allocation by their negations
     // (G[N + i] = -G[i]): a negative MSM digit gathers -G_i (MsmSeg::negofs = N)
     dev::NielsD *G = nullptr, *H = nullptr;
+    // sums of H over local index ranges [a, b) (the IPP's padding lanes in
+    // round 0, gpu_prove_lockstep): computed once per range on first use
+    mutable std::mutex sums_mu;
+    mutable std::map<std::pair<uint32_t, uint32_t>, Point> h_sums;
     ~GenSet();
 };
 // Comb tables of a generator set for the IPP's first two rounds:
@@ -186,6 +190,9 @@ struct ProducerStage {
     hipEvent_t drawn[2] = {nullptr, nullptr};   // s_L / s_R copies complete (rng_draw_group's progress)
     uint8_t *one = nullptr;                  // pinned, all draws of a one-proof group (grown)
     size_t one_cap = 0;
+    // the pinned buffers hold blinding draws (s_L, s_R): zeroed on the copy
+    // stream once their copies have landed; the next writer waits for it
+    hipEvent_t wiped = nullptr;
     ~ProducerStage();
 };
 ProducerStage &producer_stage(int device);

@@ -371,8 +371,12 @@ int bpg_ctx_set_pipeline(bpg_ctx *ctx, uint32_t producers, uint32_t lockstep,
  * [9] consumer ms proving, [10] 1 if host-bound (consumers waited more than
  * a tenth of their time after the fill), [11] free HBM at the start (GB),
  * [12] estimated GB per consumer, [13] consumers the threads allowed,
- * [14] consumers HBM admitted, [15] CPUs the process may use. */
-#define BPG_BATCH_STATS 16
+ * [14] consumers HBM admitted, [15] CPUs the process may use, [16] the
+ * hardware queues HIP gives the process (GPU_MAX_HW_QUEUES when HIP
+ * initialised, else HIP's default 4): consumers are at most that many, one
+ * stream per queue. Export GPU_MAX_HW_QUEUES=16 before anything initialises
+ * HIP for the full layout. */
+#define BPG_BATCH_STATS 17
 int bpg_last_batch_stats(double *out, int n);
 
 /* Verifier::verify (src/verify.rs:71) over `count` proofs of one circuit

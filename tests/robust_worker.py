@@ -1,5 +1,5 @@
 """Child process of tests/test_gpu_robustness.py (a fresh device context per
-run). usage: robust_worker.py cache <dir> | concurrent | exit"""
+run). usage: robust_worker.py cache <dir> | concurrent | exit | queues"""
 import json
 import os
 import sys
@@ -78,7 +78,27 @@ def exit_with_live_workspaces():
     print(json.dumps(dict(out, park=ctx.setup_stats())), flush=True)
 
 
+def queues():
+    """A batch under HIP's default hardware queues (the parent removes
+    GPU_MAX_HW_QUEUES): the library sizes its consumer streams to the queues
+    it has, and the proofs equal single proofs."""
+    import workloads as W
+    bpg = W._bpg()
+    bpg.set_seed(6)
+    syn = bpg.Synth(*W.config2())
+    ctx = bpg.Context(0)
+    prep = ctx.prepare(syn.view)
+    ents = [bytes([k + 90]) * 32 for k in range(40)]
+    proofs = prep.prove_batch(b"queues", ents, threads=14)
+    st = bpg.last_batch_stats()
+    same = all(proofs[k] == ctx.r1cs_prove(b"queues", syn.view, ents[k])[0] for k in (0, 17, 39))
+    print(json.dumps({"stats": st, "same": same, "distinct": len(set(proofs))}), flush=True)
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "queues":
+        queues()
+        sys.exit(0)
     if sys.argv[1] == "exit":
         sys.path[:0] = [ROOT]
         exit_with_live_workspaces()

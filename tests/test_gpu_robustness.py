@@ -34,8 +34,8 @@ def bpg():
     return workloads._bpg()
 
 
-def run(*args):
-    r = subprocess.run([sys.executable, WORKER] + list(args), capture_output=True, text=True, timeout=200)
+def run(*args, env=None):
+    r = subprocess.run([sys.executable, WORKER] + list(args), capture_output=True, text=True, timeout=200, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "bpg: fatal signal" not in r.stderr, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -103,3 +103,14 @@ def test_thread_exit_parks_workspace(bpg):
     assert a == b
     assert ctx.trim() >= 0
     assert ctx.setup_stats()["workspaces_parked"] == 0
+
+
+def test_batch_sizes_consumers_to_hw_queues():
+    """Without GPU_MAX_HW_QUEUES (HIP's default 4 queues) a 14-thread batch
+    runs at most 4 consumer streams and proves the same bytes as single
+    proofs (VERDICT r4 #7: the layout must not depend on bench.py's env)."""
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = run("queues", env=env)
+    st = out["stats"]
+    assert st["hw_queues"] == 4 and 1 <= st["consumers"] <= 4, st
+    assert out["same"] and out["distinct"] == 40

@@ -136,10 +136,11 @@ def test_config5_verify_batch(bpg, ctx, W):
 
 def test_config5_batch_hbm_admission(bpg, W):
     """HBM-aware admission: another allocation in the
-    process holds all but 64 GB of the free HBM and the layout asks for 28
-    proofs in flight (seven consumers of four, ~12 GB each at 2^20). The batch
-    admits fewer consumers, completes, and its proof still verifies on a fresh
-    verifier workspace afterwards (the admission keeps a verifier reserve)."""
+    process holds all but 52 GB of the free HBM and the layout asks for 28
+    proofs in flight (seven consumers of four, ~13 GB each at 2^20). The batch
+    admits fewer consumers than the threads and the hardware queues allow,
+    completes, and its proof still verifies on a fresh verifier workspace
+    afterwards (the admission keeps a verifier reserve)."""
     import torch
     inst, wit, gad = W.config5()
     bpg.set_seed(56)
@@ -149,13 +150,14 @@ def test_config5_batch_hbm_admission(bpg, W):
     prep = c.prepare(syn.view)
     prep.prove_batch(b"adm", [b"\x01" * 32], 5)   # the comb tables are built by the first batch
     free, _ = torch.cuda.mem_get_info(0)
-    hog = torch.empty(max(0, int(free - 64e9)), dtype=torch.uint8, device="cuda:0")
+    hog = torch.empty(max(0, int(free - 52e9)), dtype=torch.uint8, device="cuda:0")
     try:
         ents = [bytes([k + 7]) * 32 for k in range(40)]
         proofs = prep.prove_batch(b"adm", ents, 12)
         st = bpg.last_batch_stats()
         assert st["consumers_by_threads"] == 8
-        assert st["consumers"] == min(7, st["consumers_by_hbm"]) and st["consumers"] < 7, st
+        assert st["consumers"] == min(7, st["consumers_by_hbm"], st["hw_queues"]), st
+        assert st["consumers_by_hbm"] < min(7, st["hw_queues"]), st
         V = c.pedersen(syn.vec("v", syn.m), syn.vec("v_blinding", syn.m))
         assert c.r1cs_verify(b"adm", syn.view, V, proofs[-1])
     finally:
