@@ -119,16 +119,19 @@ void launch_gens_map(const uint8_t *uniform, NielsD *out, uint32_t count, hipStr
     BPG_HIP(hipGetLastError());
 }
 
-// signed radix-16 digit `w` of a canonical scalar (Scalar::to_radix_16)
+// signed radix-16 digit `w` of a canonical scalar (Scalar::to_radix_16).
+// Fully unrolled over the 64 nibbles with the lane's digit selected at its
+// step: a lane-dependent loop bound or word index would put s in scratch.
 DEVI int radix16_digit(const sc &s, int w) {
     int carry = 0, d = 0;
-    for (int i = 0; i <= w; i++) {
-        int nib = (s.v[i >> 3] >> (4 * (i & 7))) & 15;
-        int x = nib + carry;
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        const int nib = (s.v[i >> 3] >> (4 * (i & 7))) & 15;
+        const int x = nib + carry;
         carry = (x + 8) >> 4;
-        d = x - (carry << 4);
+        d = i == w ? x - (carry << 4) : d;
+        if (i == 63 && w == 63) d += carry << 4;   // top digit is not recentred
     }
-    if (w == 63) d += carry << 4;   // top digit is not recentred
     return d;
 }
 

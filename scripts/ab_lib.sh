@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B of library builds within one gpurun call, alternating (ABAB...):
+#   LIBS="name:path name:path ..." (path "" = the in-tree libbpg.so)
+#   scripts/ab_lib.sh <tag> [rounds] [bench args]
+# One bench line per run under gpurun_out/<tag>_<name>_<i>.json and a
+# summary table in gpurun_out/<tag>_ab.txt. Stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+T=${1:?tag}; N=${2:-2}; shift 2 || true
+ARGS=${*:---steps 5 --warmup 2 --no-cpu-baseline}
+for i in $(seq 1 $N); do
+  for v in $LIBS; do
+    name=${v%%:*}; lib=${v#*:}
+    BPG_LIB_PATH=$lib timeout -k 10 400 python3 bench.py $ARGS > gpurun_out/${T}_${name}_$i.json 2> gpurun_out/${T}_${name}_$i.err || exit $?
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/${T}_${name}_$i.json')); print('%-10s run %d  %.2f M constraints/s  %.1f ms/step  latency %.1f ms' % ('$name', $i, d['value']/1e6, d['ms_per_step'], d.get('latency_ms_single_proof') or 0))" >> gpurun_out/${T}_ab.txt
+  done
+done
+cat gpurun_out/${T}_ab.txt

@@ -1,5 +1,6 @@
 """Child process of tests/test_gpu_robustness.py (a fresh device context per
-run). usage: robust_worker.py cache <dir> | concurrent | exit | queues"""
+run). usage: robust_worker.py cache <dir> | concurrent | exit | queues |
+stmts_hbm <GB>"""
 import json
 import os
 import sys
@@ -95,7 +96,40 @@ def queues():
     print(json.dumps({"stats": st, "same": same, "distinct": len(set(proofs))}), flush=True)
 
 
+def stmts_hbm(foreign_gb):
+    """bpg_prove_statements at 12 device threads of four (16 hardware
+    queues) next to a foreign allocation of `foreign_gb` GB in this process:
+    the call must complete, or fail with an error, never abort its queues."""
+    import torch
+    import workloads as W
+    bpg = W._bpg()
+    free, _ = torch.cuda.mem_get_info(0)
+    hog = torch.empty(int(min(foreign_gb * 1e9, free - 40e9)), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    texts = [W.config5(70000 + i) for i in range(24)]
+    bpg.set_statements_layout(12, 4)
+    err = None
+    try:
+        outs = bpg.prove_statements("hbm", texts, 16)
+    except bpg.BpgError as e:
+        outs, err = [], str(e)
+    st = bpg.last_statements_stats()
+    ok = [o is not None for o in outs]
+    ver = bool(outs) and outs[-1] is not None and bpg.verify("hbm", texts[-1][0], outs[-1][0], outs[-1][1], texts[-1][2])
+    del hog
+    print(json.dumps({"proved": sum(ok), "count": len(texts), "error": err, "last_error": bpg.last_error(),
+                      "stats": st, "verified_last": ver, "foreign_gb": round(hog_bytes(foreign_gb, free) / 1e9, 1)}),
+          flush=True)
+
+
+def hog_bytes(gb, free):
+    return int(min(gb * 1e9, free - 40e9))
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "stmts_hbm":
+        stmts_hbm(float(sys.argv[2]))
+        sys.exit(0)
     if sys.argv[1] == "queues":
         queues()
         sys.exit(0)

@@ -114,3 +114,17 @@ def test_batch_sizes_consumers_to_hw_queues():
     st = out["stats"]
     assert st["hw_queues"] == 4 and 1 <= st["consumers"] <= 4, st
     assert out["same"] and out["distinct"] == 40
+
+
+def test_statements_layout_next_to_foreign_allocation():
+    """bpg_set_statements_layout(12, 4) with 16 hardware queues
+    next to a foreign 200 GB allocation completes (device threads admitted by
+    HBM) or fails cleanly -- never an aborted HSA queue. The proving kernels
+    need no scratch memory (tests/test_host.py checks the code object), so no
+    dispatch allocates device memory behind the admission's back."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    out = run("stmts_hbm", "200", env=env)
+    st = out["stats"]
+    assert out["error"] is None, out
+    assert out["proved"] == out["count"] and out["verified_last"], out
+    assert 1 <= st["consumers"] <= 12, st

@@ -131,6 +131,32 @@ def test_hot_kernels_do_not_spill(mangled, waves):
         assert int(r["Occupancy [waves/SIMD]"]) >= waves, r
 
 
+# Every kernel a default-strategy proof or a statement's prepare dispatches
+# (VERDICT r4 #6): none may need scratch memory. The HIP runtime allocates a
+# queue's scratch lazily at the first dispatch that needs it; next to a full
+# HBM that allocation failed and aborted the process's queues
+# (HSA_STATUS_ERROR_OUT_OF_RESOURCES, profiles/r04n_stmts_c16.err). Scratch-
+# free, no dispatch allocates device memory behind the HBM admission.
+# (k_bucket_seg keeps 8 B per lane: ~8 MB per queue, inside the admission's
+# reserve.)
+SCRATCH_FREE = ["k_msm_digits", "k_rs_hist", "k_rs_colscan", "k_rs_scatter", "k_rbk_pass", "k_rbk_final",
+                "k_row_reduce", "k_tpoly", "k_reduce_cols", "k_dot", "k_ipp_prep", "k_ipp_prep_lazy",
+                "k_ipp_prep_deep2", "k_ipp_prep_tail", "k_ipp_fold_scalars", "k_ipp_tail_weights",
+                "k_ipp_comb_fold", "k_ipp_fold3", "k_cached_to_niels", "k_flatten_short", "k_flatten_long",
+                "k_flatten_range", "k_gather_scalars", "k_gather_niels", "k_from_mont", "k_lr_build", "k_lr_eval",
+                "k_pow_table", "k_pow_expand", "k_wide_reduce", "k_fill_scalars", "k_pedersen", "k_decompress",
+                "k_verify_gh", "k_sc_axpy", "k_niels_neg"]
+
+
+@pytest.mark.parametrize("name", SCRATCH_FREE)
+def test_prove_path_kernels_need_no_scratch(name):
+    rows = _kernel_resources()
+    hits = [(k, v) for k, v in rows.items() if ("%d%s" % (len(name), name)) in k]
+    assert hits, name
+    for k, r in hits:
+        assert r["ScratchSize [bytes/lane]"] == "0", (k, r)
+
+
 def test_rng_selftest(bpg):
     """Host RNG (no device): the AVX-512 single-state and eight-state Keccak-f
     permutations equal the portable scalar one, TranscriptRng's 64-byte
