@@ -112,6 +112,12 @@ struct DBuf {
     size_t cap = 0;
     void grow(size_t need);
 };
+// Partial-sum buffer of the reducing kernels (dot products, t(x), c_L / c_R,
+// huge flatten columns): 8192 scalars, the launch's reduction ticket at
+// scalar RED_TICKET_WORD zeroed when (re)allocated (kernels.hip
+// block_reduce_final).
+static const unsigned RED_TICKET_WORD = 1024 * 6;
+void grow_partial(DBuf &d, hipStream_t st);
 class MsmEngine {
   public:
     explicit MsmEngine(hipStream_t st) : st_(st) {}
@@ -186,7 +192,10 @@ void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundA
                      ScD *partial, ScD *c_out, hipStream_t st);
 // acc = (first ? 0 : acc) + x * rho mod l (rho in Montgomery form)
 void launch_sc_axpy(ScD *acc, const ScD *x, uint32_t count, ScD rho_mont, bool first, hipStream_t st);
-void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st);
+// a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u (Montgomery u, u^-1) for
+// the P <= 4 proofs of a lockstep step in one launch
+void launch_ipp_fold_scalars(ScD *const *a, ScD *const *b, const ScD *u, const ScD *uinv, int P, uint32_t h,
+                             hipStream_t st);
 // Ghat' = Ghat_L + rho * Ghat_R (rho = rho_a except lanes i < n <= h+i, which use rho_b)
 // Kernel-argument block staged through pinned host memory to a device buffer
 // (one per stream; the host side is rewritten only after the stream has
@@ -269,8 +278,9 @@ void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppR
                           const ScD *wG, const ScD *wH, ScD *out, ScD *partial, ScD *c_out, hipStream_t st);
 // after round k: w_j *= rho (Montgomery) for the upper half (j mod 2h >= h),
 // rho_b for the lanes whose pair straddles n
-void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t n, ScD rGa, ScD rGb, ScD rHa,
-                             ScD rHb, hipStream_t st);
+// r[p] = {rGa, rGb, rHa, rHb} of proof p (P <= 4 proofs, one launch)
+void launch_ipp_tail_weights(ScD *const *wG, ScD *const *wH, const ScD (*r)[4], int P, uint32_t M, uint32_t h,
+                             uint32_t n, hipStream_t st);
 // verifier helpers
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
                       ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st);

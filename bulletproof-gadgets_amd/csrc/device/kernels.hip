@@ -943,6 +943,12 @@ MsmEngine::~MsmEngine() {
         if (b->p) (void)hipFree(b->p);
 }
 
+void grow_partial(DBuf &d, hipStream_t st) {
+    const size_t before = d.cap;
+    d.grow(1024 * 8 * sizeof(sc));
+    static_assert(RED_TICKET_WORD < 1024 * 8, "ticket inside the partial buffer");
+    if (d.cap != before) BPG_HIP(hipMemsetAsync(static_cast<sc *>(d.p) + RED_TICKET_WORD, 0, sizeof(sc), st));
+}
 void DBuf::grow(size_t need) {
     if (need <= cap) return;
     if (p) BPG_HIP(hipFree(p));
@@ -1395,11 +1401,69 @@ DEVI void block_reduce_store(sc (&v)[K], sc *__restrict__ partial) {
     }
 }
 #define RED_BLOCKS 1024
+// The launch's reduction ticket: a word after the partials (K <= 6 columns of
+// at most RED_BLOCKS blocks) of the caller's partial buffer, zeroed when the
+// buffer is allocated (grow_partial) and reset by each launch's last block.
+#define RED_TICKET RED_TICKET_WORD
+// Per-block partials (block_reduce_store), then the LAST block of the launch
+// to finish sums them column by column into out[k] (mode 0: Montgomery-
+// scaled partials, times R; 1: as is; 2: negated) -- one launch instead of
+// the kernel plus a k_reduce_cols launch. Hand-off per the agent-scope
+// release / acquire recipe (cdna_hip_programming.md Guideline 16, counter
+// form): every block's partial is drained and released before its ticket
+// add; the last block acquires before reading the other blocks' partials.
+template <int K>
+DEVI void block_reduce_final(sc (&v)[K], sc *__restrict__ partial, sc *__restrict__ out, int mode) {
+    block_reduce_store<K>(v, partial);
+    __shared__ sc sh[256];
+    __shared__ uint32_t last;
+    const uint32_t tid = threadIdx.x, nb = gridDim.x;
+    uint32_t *ticket = reinterpret_cast<uint32_t *>(partial + RED_TICKET);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == nb - 1 ? 1u : 0u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        sc acc;
+        sc_zero(acc);
+        for (uint32_t b = tid; b < nb; b += blockDim.x) { sc t; sc_load(t, partial + (size_t)b * K + k); sc_add(acc, acc, t); }
+        sc_store(&sh[tid], acc);
+        for (int s = 128; s >= 1; s >>= 1) {
+            __syncthreads();
+            if (tid < (uint32_t)s) { sc x, y; sc_load(x, &sh[tid]); sc_load(y, &sh[tid + s]); sc_add(x, x, y); sc_store(&sh[tid], x); }
+        }
+        if (tid == 0) {
+            sc r;
+            sc_load(r, &sh[0]);
+            if (mode == 0) {   // Montgomery-scaled partials: multiply back by R
+                sc r2;
+                for (int i = 0; i < 8; i++) r2.v[i] = SC_R2[i];
+                mm(r, r, r2);
+            } else if (mode == 2) {
+                sc_neg(r, r);
+            }
+            sc_store(out + k, r);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+}
 // Montgomery-scaled sums (sum a*b/R); the final reduce multiplies by R^2/R
 __global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const sc *__restrict__ l2,
                                                const sc *__restrict__ l3, const sc *__restrict__ r0,
                                                const sc *__restrict__ r1, const sc *__restrict__ r3, uint32_t n,
-                                               sc *__restrict__ partial) {
+                                               sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[6];
     for (int k = 0; k < 6; k++) sc_zero(acc[k]);
@@ -1414,44 +1478,18 @@ __global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const 
         mm(t, a2, b3); sc_add(acc[4], acc[4], t);                                   // t5
         mm(t, a3, b3); sc_add(acc[5], acc[5], t);                                   // t6
     }
-    block_reduce_store<6>(acc, partial);
-}
-// out[k] = R * sum_b partial[b*K + k]   (one block per k)
-__global__ __launch_bounds__(256) void k_reduce_cols(const sc *__restrict__ partial, uint32_t nb, uint32_t K,
-                                                     sc *__restrict__ out, uint32_t out_stride, int mode) {
-    WAVE_PRIO(BPG_MISC_PRIO);
-    __shared__ sc sh[256];
-    uint32_t k = blockIdx.x, tid = threadIdx.x;
-    sc acc; sc_zero(acc);
-    for (uint32_t b = tid; b < nb; b += 256) { sc t; sc_load(t, partial + (size_t)b * K + k); sc_add(acc, acc, t); }
-    sc_store(&sh[tid], acc);
-    for (int s = 128; s >= 1; s >>= 1) {
-        __syncthreads();
-        if (tid < (uint32_t)s) { sc a, b; sc_load(a, &sh[tid]); sc_load(b, &sh[tid + s]); sc_add(a, a, b); sc_store(&sh[tid], a); }
-    }
-    if (tid == 0) {
-        sc r, r2;
-        sc_load(r, &sh[0]);
-        if (mode == 0) {   // Montgomery-scaled partials: multiply back by R
-            for (int i = 0; i < 8; i++) r2.v[i] = SC_R2[i];
-            mm(r, r, r2);
-        } else if (mode == 2) {
-            sc_neg(r, r);
-        }
-        sc_store(out + (size_t)k * out_stride, r);
-    }
+    block_reduce_final<6>(acc, partial, red_out, 0);
 }
 void launch_tpoly(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, const ScD *r1, const ScD *r3,
                   uint32_t n, ScD *partial, ScD *out6, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(n, 256)));
     hipLaunchKernelGGL(k_tpoly, dim3(nb), dim3(256), 0, st, AS_CSC(l1), AS_CSC(l2), AS_CSC(l3), AS_CSC(r0),
-                       AS_CSC(r1), AS_CSC(r3), n, AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(6), dim3(256), 0, st, AS_CSC(partial), nb, 6u, AS_SC(out6), 1u, 0);
+                       AS_CSC(r1), AS_CSC(r3), n, AS_SC(partial), AS_SC(out6));
     BPG_HIP(hipGetLastError());
 }
 __global__ __launch_bounds__(256) void k_flatten_range(const sc *__restrict__ coeff, const uint32_t *__restrict__ row,
                                                        uint32_t k0, uint32_t k1, const sc *__restrict__ zlo,
-                                                       const sc *__restrict__ zhi, sc *__restrict__ partial) {
+                                                       const sc *__restrict__ zhi, sc *__restrict__ partial, sc *__restrict__ red_out, int red_mode) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[1];
     sc_zero(acc[0]);
@@ -1459,19 +1497,17 @@ __global__ __launch_bounds__(256) void k_flatten_range(const sc *__restrict__ co
         sc co; sc_load(co, coeff + k);
         flat_term(acc[0], row[k], co, zlo, zhi);
     }
-    block_reduce_store<1>(acc, partial);
+    block_reduce_final<1>(acc, partial, red_out, red_mode);
 }
 void launch_flatten_huge(const CscDev &csc, uint32_t col, uint32_t k0, uint32_t k1, const ScD *zlo, const ScD *zhi,
                          ScD *partial, ScD *out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(k1 - k0, 256)));
     hipLaunchKernelGGL(k_flatten_range, dim3(nb), dim3(256), 0, st, AS_CSC(csc.coeff), csc.row, k0, k1, AS_CSC(zlo),
-                       AS_CSC(zhi), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(256), 0, st, AS_CSC(partial), nb, 1u, AS_SC(out + col), 1u,
-                       col >= csc.neg_from ? 2 : 1);
+                       AS_CSC(zhi), AS_SC(partial), AS_SC(out + col), col >= csc.neg_from ? 2 : 1);
     BPG_HIP(hipGetLastError());
 }
 __global__ __launch_bounds__(256) void k_dot(const sc *__restrict__ a, const sc *__restrict__ b, uint32_t n,
-                                             sc *__restrict__ partial) {
+                                             sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[1];
     sc_zero(acc[0]);
@@ -1480,12 +1516,11 @@ __global__ __launch_bounds__(256) void k_dot(const sc *__restrict__ a, const sc 
         sc_load(x, a + i); sc_load(y, b + i);
         mm(t, x, y); sc_add(acc[0], acc[0], t);
     }
-    block_reduce_store<1>(acc, partial);
+    block_reduce_final<1>(acc, partial, red_out, 0);
 }
 void launch_dot(const ScD *a, const ScD *b, uint32_t n, ScD *partial, ScD *out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(n, 256)));
-    hipLaunchKernelGGL(k_dot, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), n, AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(256), 0, st, AS_CSC(partial), nb, 1u, AS_SC(out), 1u, 0);
+    hipLaunchKernelGGL(k_dot, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), n, AS_SC(partial), AS_SC(out));
     BPG_HIP(hipGetLastError());
 }
 
@@ -1526,7 +1561,7 @@ void launch_lr_eval(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, 
 // ===========================================================================
 __global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, const sc *__restrict__ b,
                                                   const sc *__restrict__ yipm, IppRoundArgs A, sc *__restrict__ out,
-                                                  sc *__restrict__ partial) {
+                                                  sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
@@ -1546,22 +1581,26 @@ __global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, cons
         mm(t, aR, lo_real ? lamG1 : lamGu); sc_store(out + 2 * h + i, t);
         sc_load(y, yipm + h + i); mm(t, bL, y); mm(t, t, hi_real ? muH1 : muHu); sc_store(out + 3 * h + i, t);
     }
-    block_reduce_store<2>(acc, partial);
+    block_reduce_final<2>(acc, partial, red_out, 0);
 }
 void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
                      ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
     hipLaunchKernelGGL(k_ipp_prep, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args,
-                       AS_SC(msm_scal), AS_SC(partial));
+                       AS_SC(msm_scal), AS_SC(partial), AS_SC(c_out));
     // c_L -> c_out[0], c_R -> c_out[1]
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
     BPG_HIP(hipGetLastError());
 }
 // u, uinv in Montgomery form
-__global__ void k_ipp_fold_scalars(sc *__restrict__ a, sc *__restrict__ b, uint32_t h, sc um, sc uim) {
+struct FoldScalarsArgs { sc *a[4], *b[4]; sc um[4], uim[4]; };
+// a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u for the P proofs of a
+// lockstep step (blockIdx.y = proof): one launch per round, not one per proof
+__global__ void k_ipp_fold_scalars(FoldScalarsArgs A, uint32_t h) {
     WAVE_PRIO(BPG_MISC_PRIO);
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
     if (i >= h) return;
+    sc *a = A.a[p], *b = A.b[p];
+    const sc um = A.um[p], uim = A.uim[p];
     sc x, y, t1, t2;
     sc_load(x, a + i); sc_load(y, a + h + i); mm(t1, x, um); mm(t2, y, uim); sc_add(t1, t1, t2); sc_store(a + i, t1);
     sc_load(x, b + i); sc_load(y, b + h + i); mm(t1, x, uim); mm(t2, y, um); sc_add(t1, t1, t2); sc_store(b + i, t1);
@@ -1585,9 +1624,15 @@ void launch_sc_axpy(ScD *acc, const ScD *x, uint32_t count, ScD rho_mont, bool f
                        *reinterpret_cast<sc *>(&rho_mont), first ? 1 : 0);
     BPG_HIP(hipGetLastError());
 }
-void launch_ipp_fold_scalars(ScD *a, ScD *b, uint32_t h, ScD u, ScD uinv, hipStream_t st) {
-    hipLaunchKernelGGL(k_ipp_fold_scalars, dim3(nblk(h, 256)), dim3(256), 0, st, AS_SC(a), AS_SC(b), h,
-                       *reinterpret_cast<sc *>(&u), *reinterpret_cast<sc *>(&uinv));
+void launch_ipp_fold_scalars(ScD *const *a, ScD *const *b, const ScD *u, const ScD *uinv, int P, uint32_t h,
+                             hipStream_t st) {
+    if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "fold scalars proofs", __FILE__, __LINE__);
+    FoldScalarsArgs A{};
+    for (int p = 0; p < P; p++) {
+        A.a[p] = AS_SC(a[p]); A.b[p] = AS_SC(b[p]);
+        A.um[p] = *reinterpret_cast<const sc *>(&u[p]); A.uim[p] = *reinterpret_cast<const sc *>(&uinv[p]);
+    }
+    hipLaunchKernelGGL(k_ipp_fold_scalars, dim3(nblk(h, 256), P), dim3(256), 0, st, A, h);
     BPG_HIP(hipGetLastError());
 }
 // Point fold: out_i = P_L,i + rho * P_R,i with one rho per lane class. rho is
@@ -2352,7 +2397,7 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
 // c_R at 8h+1. rho0 classes as in the fold (pair straddles n -> *_b).
 __global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a, const sc *__restrict__ b,
                                                        const sc *__restrict__ yipm, IppRoundArgs A, LazyArgs Z,
-                                                       sc *__restrict__ out, sc *__restrict__ partial) {
+                                                       sc *__restrict__ out, sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
@@ -2382,14 +2427,13 @@ __global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a,
         sc_load(y, yipm + hi); mm(t, bL, y); mm(t, t, hi_real ? muH1 : muHu); sc_store(out + 6 * h + i, t);
         mm(u, t, hi_b ? rHb : rHa); sc_store(out + 7 * h + i, u);
     }
-    block_reduce_store<2>(acc, partial);
+    block_reduce_final<2>(acc, partial, red_out, 0);
 }
 void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
                           ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
     hipLaunchKernelGGL(k_ipp_prep_lazy, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, lz,
-                       AS_SC(msm_scal), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
+                       AS_SC(msm_scal), AS_SC(partial), AS_SC(c_out));
     BPG_HIP(hipGetLastError());
 }
 
@@ -2402,7 +2446,7 @@ void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppR
 // out[(4 f + t) h + i]; c_L -> out[16h], c_R -> out[16h + 1].
 __global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a, const sc *__restrict__ b,
                                                         const sc *__restrict__ yipm, IppRoundArgs A, Deep2Args Z,
-                                                        sc *__restrict__ out, sc *__restrict__ partial) {
+                                                        sc *__restrict__ out, sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
@@ -2443,20 +2487,19 @@ __global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a
             mm(u, s, r0x); sc_store(o + 2 * (size_t)h, u);
         }
     }
-    block_reduce_store<2>(acc, partial);
+    block_reduce_final<2>(acc, partial, red_out, 0);
 }
 void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
                            ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
     hipLaunchKernelGGL(k_ipp_prep_deep2, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, z,
-                       AS_SC(msm_scal), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
+                       AS_SC(msm_scal), AS_SC(partial), AS_SC(c_out));
     BPG_HIP(hipGetLastError());
 }
 __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a, const sc *__restrict__ b,
                                                        const sc *__restrict__ yipm, IppRoundArgs A, uint32_t M,
                                                        const sc *__restrict__ wG, const sc *__restrict__ wH,
-                                                       sc *__restrict__ out, sc *__restrict__ partial) {
+                                                       sc *__restrict__ out, sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
     sc_zero(acc[0]); sc_zero(acc[1]);
@@ -2494,34 +2537,38 @@ __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a,
             sc_store(out + (size_t)M + j, z); sc_store(out + 3 * (size_t)M + j, u);
         }
     }
-    block_reduce_store<2>(acc, partial);
+    block_reduce_final<2>(acc, partial, red_out, 0);
 }
 void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, uint32_t M,
                           const ScD *wG, const ScD *wH, ScD *out, ScD *partial, ScD *c_out, hipStream_t st) {
     uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(M, 256)));
     hipLaunchKernelGGL(k_ipp_prep_tail, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, M,
-                       AS_CSC(wG), AS_CSC(wH), AS_SC(out), AS_SC(partial));
-    hipLaunchKernelGGL(k_reduce_cols, dim3(2), dim3(256), 0, st, AS_CSC(partial), nb, 2u, AS_SC(c_out), 1u, 0);
+                       AS_CSC(wG), AS_CSC(wH), AS_SC(out), AS_SC(partial), AS_SC(c_out));
     BPG_HIP(hipGetLastError());
 }
-__global__ void k_ipp_tail_weights(sc *__restrict__ wG, sc *__restrict__ wH, uint32_t M, uint32_t h, uint32_t n,
-                                   sc rGa, sc rGb, sc rHa, sc rHb) {
+struct TailWeightArgs { sc *wG[4], *wH[4]; sc r[4][4]; };   // per proof: rGa, rGb, rHa, rHb
+__global__ void k_ipp_tail_weights(TailWeightArgs A, uint32_t M, uint32_t h, uint32_t n) {
     WAVE_PRIO(BPG_MISC_PRIO);
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
     if (j >= M) return;
     const uint32_t i = j % (2 * h);
     if (i < h) return;
     const uint32_t il = i - h;
     const bool bcls = il < n && il + h >= n;
+    sc *wG = A.wG[p], *wH = A.wH[p];
     sc w;
-    sc_load(w, wG + j); mm(w, w, bcls ? rGb : rGa); sc_store(wG + j, w);
-    sc_load(w, wH + j); mm(w, w, bcls ? rHb : rHa); sc_store(wH + j, w);
+    sc_load(w, wG + j); mm(w, w, A.r[p][bcls ? 1 : 0]); sc_store(wG + j, w);
+    sc_load(w, wH + j); mm(w, w, A.r[p][bcls ? 3 : 2]); sc_store(wH + j, w);
 }
-void launch_ipp_tail_weights(ScD *wG, ScD *wH, uint32_t M, uint32_t h, uint32_t n, ScD rGa, ScD rGb, ScD rHa,
-                             ScD rHb, hipStream_t st) {
-    hipLaunchKernelGGL(k_ipp_tail_weights, dim3(nblk(M, 256)), dim3(256), 0, st, AS_SC(wG), AS_SC(wH), M, h, n,
-                       *reinterpret_cast<sc *>(&rGa), *reinterpret_cast<sc *>(&rGb), *reinterpret_cast<sc *>(&rHa),
-                       *reinterpret_cast<sc *>(&rHb));
+void launch_ipp_tail_weights(ScD *const *wG, ScD *const *wH, const ScD (*r)[4], int P, uint32_t M, uint32_t h,
+                             uint32_t n, hipStream_t st) {
+    if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "tail weights proofs", __FILE__, __LINE__);
+    TailWeightArgs A{};
+    for (int p = 0; p < P; p++) {
+        A.wG[p] = AS_SC(wG[p]); A.wH[p] = AS_SC(wH[p]);
+        for (int k = 0; k < 4; k++) A.r[p][k] = *reinterpret_cast<const sc *>(&r[p][k]);
+    }
+    hipLaunchKernelGGL(k_ipp_tail_weights, dim3(nblk(M, 256), P), dim3(256), 0, st, A, M, h, n);
     BPG_HIP(hipGetLastError());
 }
 
@@ -2599,13 +2646,21 @@ void launch_fb_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st
     hipLaunchKernelGGL(k_fb_build, dim3(nblk(N, 64)), dim3(64), 0, st, AS_CGEN(gens), N, AS_GEN(tab));
     BPG_HIP(hipGetLastError());
 }
-// Cached points -> affine Niels, one inversion per CTN_K points of a thread
-// (Montgomery's trick, the prefix products parked in the output slots): a
+// Cached points -> affine Niels with ONE field inversion per block of
+// CTN_T threads x CTN_K points (Montgomery's trick across the block): a
 // materialised IPP level kept as Niels makes the MSM jobs over it 7M madds
 // at pass 1's three waves per SIMD, instead of 8M cached additions at two.
 // From (Y+X, Y-X, 2Z, 2dT): with zi = 2 / (2Z), y+x = (Y+X) zi, y-x =
-// (Y-X) zi, 2dxy = 2dT zi. About 6M per point plus 265M / CTN_K.
-static constexpr uint32_t CTN_K = 32;
+// (Y-X) zi, 2dxy = 2dT zi.
+// Each thread multiplies its CTN_K denominators (prefix products kept in
+// registers); the threads' products are scanned across the block -- wave
+// prefix and suffix products by lane shuffles, waves combined through LDS --
+// so that 1 / (thread product) = (1 / block product) x (product of the
+// threads before) x (product of the threads after); wave 0 inverts the block
+// product while the other waves wait. Per point about 9M + 265M / 1024, and
+// every lane busy (round 4's kernel ran one serial 32-point chain per thread:
+// 0.05 waves per SIMD, profiles/r04q_pmc_table.md).
+static constexpr uint32_t CTN_T = 256, CTN_K = 4, CTN_B = CTN_T * CTN_K;
 DEVI void fe_load_g(fe &r, const uint32_t *w) {
 #pragma unroll
     for (int k = 0; k < 10; k++) r.v[k] = w[k];
@@ -2614,43 +2669,105 @@ DEVI void fe_store_g(uint32_t *w, const fe &a) {
 #pragma unroll
     for (int k = 0; k < 10; k++) w[k] = a.v[k];
 }
-__global__ __launch_bounds__(64) void k_cached_to_niels(const gec *__restrict__ in, gen *__restrict__ out,
-                                                         uint32_t count) {
+DEVI void fe_shfl_up(fe &r, const fe &a, int d) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) r.v[k] = (uint32_t)__shfl_up((int)a.v[k], d, 64);
+}
+// keep a wave-uniform field element in vector registers (else the compiler
+// runs its arithmetic on the scalar unit and spills SGPRs to scratch)
+DEVI void fe_in_vgprs(fe &r) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) asm volatile("" : "+v"(r.v[k]));
+}
+DEVI void fe_shfl_down(fe &r, const fe &a, int d) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) r.v[k] = (uint32_t)__shfl_down((int)a.v[k], d, 64);
+}
+__global__ __launch_bounds__(CTN_T) void k_cached_to_niels(const gec *__restrict__ in, gen *__restrict__ out,
+                                                           uint32_t count) {
     WAVE_PRIO(BPG_MISC_PRIO);
-    const uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * CTN_K;
-    if (i0 >= count) return;
-    const uint32_t n = (uint32_t)min<uint64_t>(CTN_K, count - i0);
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(in + i0);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(out + i0);
-    constexpr int SW = sizeof(gec) / 4, DW = sizeof(gen) / 4;   // words per point
-    fe acc, z;
-    fe_one(acc);
-    for (uint32_t k = 0; k < n; k++) {      // prefix products of 2Z, parked in out[k]
-        fe_store_g(dst + k * DW, acc);
-        fe_load_g(z, src + k * SW + 20);
-        fe_mul(acc, acc, z);
+    __shared__ fe wprod[CTN_T / 64];   // each wave's product
+    __shared__ fe binv;                // 1 / block product
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * CTN_B;
+    constexpr int SW = sizeof(gec) / 4;
+    // this thread's points: base + k CTN_T + t (coalesced across the block);
+    // q_k = product of its denominators 0..k (past the end: 1). Named
+    // registers, not an array: the compiler put a q[] array in scratch.
+    static_assert(CTN_K == 4, "the walk below is written out for four points");
+    auto den = [&](int k, fe &z) {
+        const uint64_t i = base + (uint64_t)k * CTN_T + t;
+        if (i < count) fe_load_g(z, reinterpret_cast<const uint32_t *>(in + i) + 20);
+        else fe_one(z);
+    };
+    fe q0, q1, q2, z;
+    den(0, q0);
+    den(1, z); fe_mul(q1, q0, z);
+    den(2, z); fe_mul(q2, q1, z);
+    den(3, z);
+    fe p;
+    fe_mul(p, q2, z);
+
+    // inclusive prefix (pre) and suffix (suf) products of p within the wave
+    fe pre = p, suf = p, o;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        fe_shfl_up(o, pre, d);
+        fe_mul(o, o, pre);
+        if (lane >= (uint32_t)d) pre = o;
+        fe_shfl_down(o, suf, d);
+        fe_mul(o, o, suf);
+        if (lane + d < 64) suf = o;
     }
-    fe inv;
-    fe_invert(inv, acc);
-    for (int k = (int)n - 1; k >= 0; k--) {
-        fe pre, zi, t;
-        fe_load_g(pre, dst + k * DW);
-        fe_mul(zi, inv, pre);                // 1 / (2Z_k)
-        fe_load_g(z, src + k * SW + 20);
-        fe_mul(inv, inv, z);
-        fe_add(zi, zi, zi);                  // 1 / Z_k
+    if (lane == 63) wprod[wv] = pre;
+    __syncthreads();
+    // products of the threads before (ex_pre) and after (ex_suf) this one
+    fe ex_pre, ex_suf;
+    fe_shfl_up(ex_pre, pre, 1);
+    fe_shfl_down(ex_suf, suf, 1);
+    if (lane == 0) fe_one(ex_pre);
+    if (lane == 63) fe_one(ex_suf);
+    for (uint32_t j = 0; j < wv; j++) fe_mul(ex_pre, ex_pre, wprod[j]);
+    for (uint32_t j = wv + 1; j < CTN_T / 64; j++) fe_mul(ex_suf, ex_suf, wprod[j]);
+    if (wv == 0) {   // one wave inverts the block product
+        fe tot = wprod[0];
+        fe_in_vgprs(tot);
+#pragma unroll
+        for (uint32_t j = 1; j < CTN_T / 64; j++) fe_mul(tot, tot, wprod[j]);
+        fe inv;
+        fe_invert(inv, tot);
+        if (lane == 0) binv = inv;
+    }
+    __syncthreads();
+    fe inv, bi = binv;   // 1 / p
+    fe_in_vgprs(bi);
+    fe_mul(inv, bi, ex_pre);
+    fe_mul(inv, inv, ex_suf);
+    // walk back through the thread's own points: 1 / (2Z_k) = inv_k q_(k-1),
+    // inv_(k-1) = inv_k 2Z_k
+    auto emit = [&](int k, fe zi) {   // zi = 1 / (2Z_k)
+        const uint64_t i = base + (uint64_t)k * CTN_T + t;
+        if (i >= count) return;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(in + i);
+        fe_add(zi, zi, zi);                       // 1 / Z_k
         gen g;
-        fe_load_g(t, src + k * SW);      fe_mul(g.YpX, t, zi);
-        fe_load_g(t, src + k * SW + 10); fe_mul(g.YmX, t, zi);
-        fe_load_g(t, src + k * SW + 30); fe_mul(g.T2d, t, zi);
+        fe tt;
+        fe_load_g(tt, src);      fe_mul(g.YpX, tt, zi);
+        fe_load_g(tt, src + 10); fe_mul(g.YmX, tt, zi);
+        fe_load_g(tt, src + 30); fe_mul(g.T2d, tt, zi);
         g.pad[0] = g.pad[1] = 0;
-        gen_store(out + i0 + k, g);
-    }
+        gen_store(out + i, g);
+    };
+    fe zi;
+    fe_mul(zi, inv, q2); emit(3, zi); den(3, z); fe_mul(inv, inv, z);
+    fe_mul(zi, inv, q1); emit(2, zi); den(2, z); fe_mul(inv, inv, z);
+    fe_mul(zi, inv, q0); emit(1, zi); den(1, z); fe_mul(inv, inv, z);
+    emit(0, inv);
 }
 void launch_cached_to_niels(const PtD *in, NielsD *out, uint32_t count, hipStream_t st) {
     if (!count) return;
-    const uint32_t thr = (count + CTN_K - 1) / CTN_K;
-    hipLaunchKernelGGL(k_cached_to_niels, dim3(nblk(thr, 64)), dim3(64), 0, st, AS_CGEC(in), AS_GEN(out), count);
+    hipLaunchKernelGGL(k_cached_to_niels, dim3((count + CTN_B - 1) / CTN_B), dim3(CTN_T), 0, st, AS_CGEC(in),
+                       AS_GEN(out), count);
     BPG_HIP(hipGetLastError());
 }
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st) {

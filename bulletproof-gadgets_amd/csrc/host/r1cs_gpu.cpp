@@ -1436,7 +1436,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
         B.w.grow((size_t)cp.ncol * sizeof(ScD) + 64);
         int pfl = ws.prof_begin("flatten", (double)cp.ncol * 32);
         launch_flatten(csc, as<ScD>(B.zlo), as<ScD>(B.zhi), as<ScD>(B.w), st);
-        B.partial.grow(1024 * 8 * sizeof(ScD));
+        grow_partial(B.partial, st);
         for (uint32_t col : cp.huge_cols)
             launch_flatten_huge(csc, col, cp.col_ptr_host[col], cp.col_ptr_host[col + 1], as<ScD>(B.zlo),
                                 as<ScD>(B.zhi), as<ScD>(B.partial), as<ScD>(B.w), st);
@@ -1684,6 +1684,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
         ws.prof_end(ph);
         ws.sync();
         std::vector<std::array<Scalar, 4>> rnow(P);   // this round's fold scalars (G a/b, H a/b)
+        ScD *fa[MAX_LOCKSTEP], *fb[MAX_LOCKSTEP], fu[MAX_LOCKSTEP], fui[MAX_LOCKSTEP];   // a, b folds
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             Point LR[2], cq;
@@ -1711,19 +1712,24 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             T[p].append_point("R", cr);
             const Scalar uk = T[p].challenge_scalar("u");
             const Scalar uinv = sc_invert(uk);
-            launch_ipp_fold_scalars(as<ScD>(B.a), as<ScD>(B.b), h, mont(uk), mont(uinv), st);
+            fa[p] = as<ScD>(B.a); fb[p] = as<ScD>(B.b); fu[p] = mont(uk); fui[p] = mont(uinv);
             const Scalar u2 = uk * uk, ui2 = uinv * uinv;
             const Scalar yh = sc_pow_u64(y_inv[p], (uint64_t)h * world);   // the round's global half length
             rnow[p] = {u2, u2 * u[p], ui2 * yh, ui2 * yh * u[p]};
             lam[p] = lam[p] * uinv;
             mu[p] = mu[p] * uk;
         }
+        launch_ipp_fold_scalars(fa, fb, fu, fui, P, h, st);   // the round's a, b folds of every proof
         const int nxt = cur == 0 ? 1 : 0;
         if (tail) {
-            if (h > 1 || sharded)
-                for (int p = 0; p < P; p++)
-                    launch_ipp_tail_weights(as<ScD>(ws.pb[p].wG), as<ScD>(ws.pb[p].wH), M, h, nl, mont(rnow[p][0]),
-                                            mont(rnow[p][1]), mont(rnow[p][2]), mont(rnow[p][3]), st);
+            if (h > 1 || sharded) {
+                ScD *wg[MAX_LOCKSTEP], *wh[MAX_LOCKSTEP], rw[MAX_LOCKSTEP][4];
+                for (int p = 0; p < P; p++) {
+                    wg[p] = as<ScD>(ws.pb[p].wG); wh[p] = as<ScD>(ws.pb[p].wH);
+                    for (int q = 0; q < 4; q++) rw[p][q] = mont(rnow[p][q]);
+                }
+                launch_ipp_tail_weights(wg, wh, rw, P, M, h, nl, st);
+            }
         } else if (h > 1) {
             const int group = (comb && cur < 0) ? 2 : group_cfg;
             if (depth + 1 < group) {   // level k + depth + 1 stays implicit
@@ -2034,7 +2040,7 @@ static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label
                as<ScD>(const_cast<DBuf &>(cs.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cs.short_cols)),
                as<uint32_t>(const_cast<DBuf &>(cs.long_cols)), cs.nshort, cs.nlong, cs.ncol, 3 * n};
     launch_flatten(csc, as<ScD>(ws.zlo), as<ScD>(ws.zhi), as<ScD>(ws.w), st);
-    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    grow_partial(ws.partial, st);
     for (uint32_t col : cs.huge_cols)
         launch_flatten_huge(csc, col, cs.col_ptr_host[col], cs.col_ptr_host[col + 1], as<ScD>(ws.zlo), as<ScD>(ws.zhi),
                             as<ScD>(ws.partial), as<ScD>(ws.w), st);
@@ -2067,7 +2073,7 @@ static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label
     ws.ynwR.grow((size_t)(n ? n : 1) * sizeof(ScD) + 64);
     launch_verify_gh(as<ScD>(ws.w), as<ScD>(ws.yipm), u2d, to_dev(allinv), n, N, lgn, mont(x), mont(pa), mont(pb),
                      mont(u), gh, as<ScD>(ws.ynwR), st);
-    ws.partial.grow(1024 * 8 * sizeof(ScD));
+    grow_partial(ws.partial, st);
     ScD *dsm = u2d + 40;
     if (n) launch_dot(as<ScD>(ws.ynwR), as<ScD>(ws.w), n, as<ScD>(ws.partial), dsm, st);
     else BPG_HIP(hipMemsetAsync(dsm, 0, sizeof(ScD), st));

@@ -140,7 +140,7 @@ def test_hot_kernels_do_not_spill(mangled, waves):
 # (k_bucket_seg keeps 8 B per lane: ~8 MB per queue, inside the admission's
 # reserve.)
 SCRATCH_FREE = ["k_msm_digits", "k_rs_hist", "k_rs_colscan", "k_rs_scatter", "k_rbk_pass", "k_rbk_final",
-                "k_row_reduce", "k_tpoly", "k_reduce_cols", "k_dot", "k_ipp_prep", "k_ipp_prep_lazy",
+                "k_row_reduce", "k_tpoly", "k_dot", "k_ipp_prep", "k_ipp_prep_lazy",
                 "k_ipp_prep_deep2", "k_ipp_prep_tail", "k_ipp_fold_scalars", "k_ipp_tail_weights",
                 "k_ipp_comb_fold", "k_ipp_fold3", "k_cached_to_niels", "k_flatten_short", "k_flatten_long",
                 "k_flatten_range", "k_gather_scalars", "k_gather_niels", "k_from_mont", "k_lr_build", "k_lr_eval",
