@@ -59,7 +59,8 @@ ProfSink *prof_sink();
 // out[i] = -in[i] (affine Niels: swap y+x / y-x, negate 2dxy)
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = in[i] as affine Niels (cached in; one inversion per 32 points)
-void launch_cached_to_niels(const PtD *in, NielsD *out, uint32_t count, hipStream_t st);
+// cached -> affine Niels for nvec <= 8 vectors of `count` points each, one launch
+void launch_cached_to_niels(const PtD *const *in, NielsD *const *out, int nvec, uint32_t count, hipStream_t st);
 // out[i] = from_uniform_bytes(uniform[64*i .. 64*i+64))
 void launch_gens_map(const uint8_t *uniform, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = v[i]*B + vb[i]*B_blinding using fixed-base tables (64 x 8 points each)
@@ -188,8 +189,6 @@ struct IppRoundArgs {
 // msm_scal[0..4h) = [aL*lamGf_R | bR*muHf_L | aR*lamGf_L | bL*muHf_R]; c_L -> msm_scal[4h],
 // c_R -> msm_scal[4h+1]
 // c_out: c_L, c_R (2 scalars; may be a device view of pinned host memory)
-void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
-                     ScD *partial, ScD *c_out, hipStream_t st);
 // acc = (first ? 0 : acc) + x * rho mod l (rho in Montgomery form)
 void launch_sc_axpy(ScD *acc, const ScD *x, uint32_t count, ScD rho_mont, bool first, hipStream_t st);
 // a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u (Montgomery u, u^-1) for
@@ -249,8 +248,6 @@ struct LazyArgs {
     ScD rGa, rGb, rHa, rHb;   // round-0 fold scalars (Montgomery), per class
 };
 // msm_scal[0..8h) (layout in kernels.hip), c_L -> [8h], c_R -> [8h+1]
-void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
-                          ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st);
 // Round k+2 of a round triple (levels k+1, k+2 unmaterialised): each base
 // expanded into four level-k points. r1/r0: rounds k+1 / k fold scalars
 // (Montgomery) per vector (0 = G, 1 = H) and class (1: the pair straddles n).
@@ -258,8 +255,24 @@ struct Deep2Args {
     ScD r1[2][2], r0[2][2];
 };
 // msm_scal[0..16h) (layout in kernels.hip), c_L -> [16h], c_R -> [16h+1]
-void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
-                           ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st);
+// The IPP round preparation of the P <= 4 proofs of a lockstep step, one
+// launch: kind PREP_PLAIN (msm_scal[0..4h) = [aL*lamGf_R | bR*muHf_L |
+// aR*lamGf_L | bL*muHf_R]), PREP_LAZY (8h scalars, bases one level above the
+// materialised one), PREP_DEEP2 (16h, two levels above), PREP_TAIL (4M, the
+// tail's weighted bases); per proof c_L -> c_out[0], c_R -> c_out[1] (may be
+// a device view of pinned host memory). h (A[p].h) and M are the same for
+// every proof of the step.
+enum { PREP_PLAIN = 0, PREP_LAZY = 1, PREP_DEEP2 = 2, PREP_TAIL = 3 };
+struct PrepBatch {
+    const ScD *a[4], *b[4], *yipm[4];
+    ScD *out[4], *partial[4], *c_out[4];
+    IppRoundArgs A[4];
+    LazyArgs lz[4];
+    Deep2Args dz[4];
+    const ScD *wG[4], *wH[4];
+    uint32_t M;
+};
+void launch_ipp_prep(const PrepBatch &B, int kind, int P, hipStream_t st);
 // Three-round Straus fold from level k (NielsD at level 0, else PtD):
 // out_i = P_i + sum_{t=1..7} c_t P_{i + t hq}, i < hq; coef[v][r][t-1] canonical
 // for lanes [rstart[r], rstart[r+1]). `tab`: odd-multiple tables,
@@ -274,8 +287,6 @@ void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq,
 // sum over j = i mod 2h of w_j P_j. The round's L/R job is 4 segments of M
 // scalars over that level: out = [sLG | sLH | sRG | sRH] (a point not in a
 // segment's half gets 0), c_L -> out[4M], c_R -> out[4M + 1].
-void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, uint32_t M,
-                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, ScD *c_out, hipStream_t st);
 // after round k: w_j *= rho (Montgomery) for the upper half (j mod 2h >= h),
 // rho_b for the lanes whose pair straddles n
 // r[p] = {rGa, rGb, rHa, rHb} of proof p (P <= 4 proofs, one launch)

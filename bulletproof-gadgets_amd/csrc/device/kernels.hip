@@ -1559,8 +1559,8 @@ void launch_lr_eval(const ScD *l1, const ScD *l2, const ScD *l3, const ScD *r0, 
 // ===========================================================================
 // IPP
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, const sc *__restrict__ b,
-                                                  const sc *__restrict__ yipm, IppRoundArgs A, sc *__restrict__ out,
+DEVI void ipp_prep_body(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                  const sc *__restrict__ yipm, const IppRoundArgs &A, sc *__restrict__ out,
                                                   sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
@@ -1582,14 +1582,6 @@ __global__ __launch_bounds__(256) void k_ipp_prep(const sc *__restrict__ a, cons
         sc_load(y, yipm + h + i); mm(t, bL, y); mm(t, t, hi_real ? muH1 : muHu); sc_store(out + 3 * h + i, t);
     }
     block_reduce_final<2>(acc, partial, red_out, 0);
-}
-void launch_ipp_prep(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, ScD *msm_scal,
-                     ScD *partial, ScD *c_out, hipStream_t st) {
-    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
-    hipLaunchKernelGGL(k_ipp_prep, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args,
-                       AS_SC(msm_scal), AS_SC(partial), AS_SC(c_out));
-    // c_L -> c_out[0], c_R -> c_out[1]
-    BPG_HIP(hipGetLastError());
 }
 // u, uinv in Montgomery form
 struct FoldScalarsArgs { sc *a[4], *b[4]; sc um[4], uim[4]; };
@@ -2395,8 +2387,8 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
 // two level-0 generators, so the round's MSM scalars double (8h of them).
 // Layout: [L: G_A | G_B | H_A | H_B | R: G_A | G_B | H_A | H_B], c_L at 8h,
 // c_R at 8h+1. rho0 classes as in the fold (pair straddles n -> *_b).
-__global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a, const sc *__restrict__ b,
-                                                       const sc *__restrict__ yipm, IppRoundArgs A, LazyArgs Z,
+DEVI void ipp_prep_lazy_body(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                       const sc *__restrict__ yipm, const IppRoundArgs &A, const LazyArgs &Z,
                                                        sc *__restrict__ out, sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
@@ -2429,13 +2421,6 @@ __global__ __launch_bounds__(256) void k_ipp_prep_lazy(const sc *__restrict__ a,
     }
     block_reduce_final<2>(acc, partial, red_out, 0);
 }
-void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const LazyArgs &lz,
-                          ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st) {
-    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
-    hipLaunchKernelGGL(k_ipp_prep_lazy, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, lz,
-                       AS_SC(msm_scal), AS_SC(partial), AS_SC(c_out));
-    BPG_HIP(hipGetLastError());
-}
 
 // IPP tail round over the materialised level (M points per vector).
 // Round k+2 of a round triple: each level-(k+2) base x (2h of them per
@@ -2444,8 +2429,8 @@ void launch_ipp_prep_lazy(const ScD *a, const ScD *b, const ScD *yip, const IppR
 // scalar (class: x < n <= x + 2h), r0 the round-k one (class: y < n <= y + 4h).
 // Layout: family f in [L: G_hi, H_lo | R: G_lo, H_hi], term t:
 // out[(4 f + t) h + i]; c_L -> out[16h], c_R -> out[16h + 1].
-__global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a, const sc *__restrict__ b,
-                                                        const sc *__restrict__ yipm, IppRoundArgs A, Deep2Args Z,
+DEVI void ipp_prep_deep2_body(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                        const sc *__restrict__ yipm, const IppRoundArgs &A, const Deep2Args &Z,
                                                         sc *__restrict__ out, sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
     sc acc[2];
@@ -2489,15 +2474,8 @@ __global__ __launch_bounds__(256) void k_ipp_prep_deep2(const sc *__restrict__ a
     }
     block_reduce_final<2>(acc, partial, red_out, 0);
 }
-void launch_ipp_prep_deep2(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, const Deep2Args &z,
-                           ScD *msm_scal, ScD *partial, ScD *c_out, hipStream_t st) {
-    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(args.h, 256)));
-    hipLaunchKernelGGL(k_ipp_prep_deep2, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, z,
-                       AS_SC(msm_scal), AS_SC(partial), AS_SC(c_out));
-    BPG_HIP(hipGetLastError());
-}
-__global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a, const sc *__restrict__ b,
-                                                       const sc *__restrict__ yipm, IppRoundArgs A, uint32_t M,
+DEVI void ipp_prep_tail_body(const sc *__restrict__ a, const sc *__restrict__ b,
+                                                       const sc *__restrict__ yipm, const IppRoundArgs &A, uint32_t M,
                                                        const sc *__restrict__ wG, const sc *__restrict__ wH,
                                                        sc *__restrict__ out, sc *__restrict__ partial, sc *__restrict__ red_out) {
     WAVE_PRIO(BPG_MISC_PRIO);
@@ -2539,11 +2517,39 @@ __global__ __launch_bounds__(256) void k_ipp_prep_tail(const sc *__restrict__ a,
     }
     block_reduce_final<2>(acc, partial, red_out, 0);
 }
-void launch_ipp_prep_tail(const ScD *a, const ScD *b, const ScD *yip, const IppRoundArgs &args, uint32_t M,
-                          const ScD *wG, const ScD *wH, ScD *out, ScD *partial, ScD *c_out, hipStream_t st) {
-    uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(M, 256)));
-    hipLaunchKernelGGL(k_ipp_prep_tail, dim3(nb), dim3(256), 0, st, AS_CSC(a), AS_CSC(b), AS_CSC(yip), args, M,
-                       AS_CSC(wG), AS_CSC(wH), AS_SC(out), AS_SC(partial), AS_SC(c_out));
+// One launch per IPP round for the P <= 4 proofs of a lockstep step
+// (blockIdx.y = proof): the round preparation's scalars and its c_L / c_R
+// (each proof's reduction finished by the last of its blocks).
+__global__ __launch_bounds__(256) void k_ipp_prep(PrepBatch B) {
+    const uint32_t p = blockIdx.y;
+    ipp_prep_body(AS_CSC(B.a[p]), AS_CSC(B.b[p]), AS_CSC(B.yipm[p]), B.A[p], AS_SC(B.out[p]), AS_SC(B.partial[p]),
+                  AS_SC(B.c_out[p]));
+}
+__global__ __launch_bounds__(256) void k_ipp_prep_lazy(PrepBatch B) {
+    const uint32_t p = blockIdx.y;
+    ipp_prep_lazy_body(AS_CSC(B.a[p]), AS_CSC(B.b[p]), AS_CSC(B.yipm[p]), B.A[p], B.lz[p], AS_SC(B.out[p]),
+                       AS_SC(B.partial[p]), AS_SC(B.c_out[p]));
+}
+__global__ __launch_bounds__(256) void k_ipp_prep_deep2(PrepBatch B) {
+    const uint32_t p = blockIdx.y;
+    ipp_prep_deep2_body(AS_CSC(B.a[p]), AS_CSC(B.b[p]), AS_CSC(B.yipm[p]), B.A[p], B.dz[p], AS_SC(B.out[p]),
+                        AS_SC(B.partial[p]), AS_SC(B.c_out[p]));
+}
+__global__ __launch_bounds__(256) void k_ipp_prep_tail(PrepBatch B) {
+    const uint32_t p = blockIdx.y;
+    ipp_prep_tail_body(AS_CSC(B.a[p]), AS_CSC(B.b[p]), AS_CSC(B.yipm[p]), B.A[p], B.M, AS_CSC(B.wG[p]),
+                       AS_CSC(B.wH[p]), AS_SC(B.out[p]), AS_SC(B.partial[p]), AS_SC(B.c_out[p]));
+}
+void launch_ipp_prep(const PrepBatch &B, int kind, int P, hipStream_t st) {
+    if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "prep proofs", __FILE__, __LINE__);
+    const uint32_t len = kind == PREP_TAIL ? B.M : B.A[0].h;
+    const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(RED_BLOCKS, nblk(len, 256))), (uint32_t)P);
+    switch (kind) {
+    case PREP_PLAIN: hipLaunchKernelGGL(k_ipp_prep, grid, dim3(256), 0, st, B); break;
+    case PREP_LAZY: hipLaunchKernelGGL(k_ipp_prep_lazy, grid, dim3(256), 0, st, B); break;
+    case PREP_DEEP2: hipLaunchKernelGGL(k_ipp_prep_deep2, grid, dim3(256), 0, st, B); break;
+    default: hipLaunchKernelGGL(k_ipp_prep_tail, grid, dim3(256), 0, st, B); break;
+    }
     BPG_HIP(hipGetLastError());
 }
 struct TailWeightArgs { sc *wG[4], *wH[4]; sc r[4][4]; };   // per proof: rGa, rGb, rHa, rHb
@@ -2683,9 +2689,13 @@ DEVI void fe_shfl_down(fe &r, const fe &a, int d) {
 #pragma unroll
     for (int k = 0; k < 10; k++) r.v[k] = (uint32_t)__shfl_down((int)a.v[k], d, 64);
 }
-__global__ __launch_bounds__(CTN_T) void k_cached_to_niels(const gec *__restrict__ in, gen *__restrict__ out,
-                                                           uint32_t count) {
+// up to 8 vectors per launch (the G and H levels of a lockstep step's
+// proofs; blockIdx.y = vector)
+struct CtnArgs { const gec *in[8]; gen *out[8]; };
+__global__ __launch_bounds__(CTN_T) void k_cached_to_niels(CtnArgs V, uint32_t count) {
     WAVE_PRIO(BPG_MISC_PRIO);
+    const gec *__restrict__ in = V.in[blockIdx.y];
+    gen *__restrict__ out = V.out[blockIdx.y];
     __shared__ fe wprod[CTN_T / 64];   // each wave's product
     __shared__ fe binv;                // 1 / block product
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2764,10 +2774,13 @@ __global__ __launch_bounds__(CTN_T) void k_cached_to_niels(const gec *__restrict
     fe_mul(zi, inv, q0); emit(1, zi); den(1, z); fe_mul(inv, inv, z);
     emit(0, inv);
 }
-void launch_cached_to_niels(const PtD *in, NielsD *out, uint32_t count, hipStream_t st) {
-    if (!count) return;
-    hipLaunchKernelGGL(k_cached_to_niels, dim3((count + CTN_B - 1) / CTN_B), dim3(CTN_T), 0, st, AS_CGEC(in),
-                       AS_GEN(out), count);
+void launch_cached_to_niels(const PtD *const *in, NielsD *const *out, int nvec, uint32_t count, hipStream_t st) {
+    if (!count || nvec < 1) return;
+    if (nvec > 8) throw HipError(hipErrorInvalidValue, "niels vectors", __FILE__, __LINE__);
+    CtnArgs V{};
+    for (int v = 0; v < nvec; v++) { V.in[v] = AS_CGEC(in[v]); V.out[v] = AS_GEN(out[v]); }
+    hipLaunchKernelGGL(k_cached_to_niels, dim3((count + CTN_B - 1) / CTN_B, (uint32_t)nvec), dim3(CTN_T), 0, st, V,
+                       count);
     BPG_HIP(hipGetLastError());
 }
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st) {

@@ -700,7 +700,7 @@ static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector
 namespace {
 std::atomic<uint32_t> g_stmt_consumers(0), g_stmt_lockstep(0);   // bpg_set_statements_layout (0: defaults)
 std::mutex g_ss_mu;
-double g_ss[13] = {0};   // bpg_last_statements_stats
+double g_ss[15] = {0};   // bpg_last_statements_stats
 }  // namespace
 int bpg_prove_statements(const char *name, const char *const *instances, const char *const *witnesses,
                          const char *const *gadgets, const uint64_t *seeds, uint32_t count, uint32_t threads,
@@ -718,7 +718,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         // in lockstep (one MSM job per IPP round for all of them, as
         // bpg_prove_batch does for one circuit)
         const uint32_t l_set = g_stmt_lockstep.load();
-        const uint32_t L = l_set ? l_set : 4;
+        uint32_t L = l_set ? l_set : 4;   // lowered by the HBM admission if need be (under mu)
         const uint32_t C = std::min<uint32_t>(std::min<uint32_t>(c_set ? 12 : 5, hw_queues()),
                                               std::max<uint32_t>(1, c_set ? c_set : W / 2));
         const size_t label_len = strlen(name);
@@ -755,7 +755,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         // what HBM holds next to the consumers' workspaces, sized once the
         // first statement is prepared (until then at most W)
         uint32_t limit = 4 * W + 8 + 2 * C, hbm_limit = 0, C_eff = C;
-        double est_st = 0;
+        double est_st = 0, adm_free_b = 0;
         double synth_ms = 0, prep_ms = 0, rng_ms = 0, prove_ms = 0, widle_ms = 0, cidle_ms = 0;
         std::string first_err;
         bool fatal = false;
@@ -859,18 +859,37 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                         // less a reserve, must hold C_eff consumer workspaces
                         // of L proofs and at least C_eff L + 8 statements in
                         // flight (the rest of it bounds the in-flight limit);
-                        // consumers beyond C_eff stay idle
+                        // consumers beyond C_eff stay idle. When not even one
+                        // consumer of L fits, L is lowered (a consumer of one
+                        // proof needs about a third of one of four); when one
+                        // of one does not fit, the call fails here with an
+                        // error, before any proof allocates.
                         est_st = (double)prepared_bytes(*it->cs);
                         const double reserve = std::max<double>(2.0 * (1 << 30), total_b / 64.0);
-                        const double per_c = (double)consumer_bytes_estimate(*it->cs, (int)L);
                         // free memory now: the first prepare built the comb
                         // tables (208 GB at 2^20) if no earlier call had;
                         // this statement's own bytes count as in flight
                         size_t free_now = 0, tot_now = 0;
                         BPG_HIP(hipMemGetInfo(&free_now, &tot_now));
+                        adm_free_b = (double)free_now;
                         const double all = (double)free_now + (double)held + est_st - reserve;
-                        uint32_t c_fit = C;
-                        while (c_fit > 1 && c_fit * per_c + (c_fit * L + 8) * est_st > all) c_fit--;
+                        double per_c = 0;
+                        uint32_t c_fit = 0;
+                        for (uint32_t l = L; l >= 1 && !c_fit; l--) {
+                            per_c = (double)consumer_bytes_estimate(*it->cs, (int)l);
+                            for (uint32_t c = C; c >= 1; c--)
+                                if (c * per_c + (c * l + 8) * est_st <= all) { c_fit = c; L = l; break; }
+                        }
+                        if (!c_fit) {
+                            char msg[256];
+                            snprintf(msg, sizeof msg,
+                                     "not enough free HBM for one device thread: %.1f GB free, %.1f GB needed "
+                                     "(one proof's workspace and 9 statements in flight, %.1f GB reserve)",
+                                     free_now / 1e9, (per_c + 9 * est_st + reserve) / 1e9, reserve / 1e9);
+                            if (first_err.empty()) first_err = msg;
+                            fatal = true;
+                            c_fit = 1;
+                        }
                         C_eff = c_fit;
                         hbm_limit = (uint32_t)std::max<double>(std::min<double>(C_eff * L + 8, limit),
                                                                (all - C_eff * per_c) / est_st);
@@ -946,8 +965,9 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             const double wbusy = 1.0 - widle_ms / std::max(1e-9, wall * W);
             const double cbusy = 1.0 - cidle_ms / std::max(1e-9, wall * C_eff);
             const int bound = wbusy >= cbusy ? 1 : 2;
-            const double v[13] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
-                                  widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9};
+            const double v[15] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
+                                  widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9, (double)L,
+                                  adm_free_b / 1e9};
             std::lock_guard<std::mutex> lk(g_ss_mu);
             memcpy(g_ss, v, sizeof(v));
         }
@@ -972,7 +992,7 @@ int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep) {
 }
 int bpg_last_statements_stats(double *out, int n) {
     std::lock_guard<std::mutex> lk(g_ss_mu);
-    for (int i = 0; i < n && i < 13; i++) out[i] = g_ss[i];
+    for (int i = 0; i < n && i < 15; i++) out[i] = g_ss[i];
     return 0;
 }
 

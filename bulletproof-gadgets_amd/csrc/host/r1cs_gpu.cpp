@@ -1568,12 +1568,15 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
     // (+0.9% in the bench, profiles/r04o_ab.txt).
     auto niels_level = [&](uint32_t cnt) {
         const int oth = cur == 0 ? 1 : 0;
-        for (int p = 0; p < P; p++) {
+        const PtD *vin[2 * MAX_LOCKSTEP];
+        NielsD *vout[2 * MAX_LOCKSTEP];
+        for (int p = 0; p < P; p++) {   // every proof's G and H level in one launch
             ProofBufs &B = ws.pb[p];
-            launch_cached_to_niels(as<PtD>(B.Gp[cur]), as<NielsD>(B.Gp[oth]), cnt, st);
-            launch_cached_to_niels(as<PtD>(B.Hp[cur]), as<NielsD>(B.Hp[oth]), cnt, st);
+            vin[2 * p] = as<PtD>(B.Gp[cur]); vout[2 * p] = as<NielsD>(B.Gp[oth]);
+            vin[2 * p + 1] = as<PtD>(B.Hp[cur]); vout[2 * p + 1] = as<NielsD>(B.Hp[oth]);
             Gh[p] = B.Gp[oth].p; Hh[p] = B.Hp[oth].p;
         }
+        launch_cached_to_niels(vin, vout, 2 * P, cnt, st);
         cur = oth;
         gfmt = MSM_NIELS;
     };
@@ -1611,6 +1614,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             pad_sum = generator_range_sum(ws, *gs, nl - h, h);
         MsmSeg seg[MSM_MAX_SEGS];
         int nseg = 0;
+        PrepBatch PB{};   // the round preparation of every proof, one launch after the loop
+        int prep_kind = PREP_PLAIN;
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             IppRoundArgs A;
@@ -1619,11 +1624,14 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             A.muH1 = mont(mu[p]); A.muHu = mont(mu[p] * u[p]);
             ScD *ms = as<ScD>(B.mscal);
             ScD *cout = B.small_view + 1020;   // c_L, c_R (pinned, device view)
+            PB.a[p] = as<ScD>(B.a); PB.b[p] = as<ScD>(B.b); PB.yipm[p] = as<ScD>(B.yipm);
+            PB.out[p] = ms; PB.partial[p] = as<ScD>(B.partial); PB.c_out[p] = cout;
+            PB.A[p] = A;
             const void *Gm = cur < 0 ? G0 : Gh[p], *Hm = cur < 0 ? H0 : Hh[p];
             const uint32_t L0 = 2 * (uint32_t)p, R0 = L0 + 1;   // this proof's L and R MSMs
             if (tail) {
-                launch_ipp_prep_tail(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, M, as<ScD>(B.wG),
-                                     as<ScD>(B.wH), ms, as<ScD>(B.partial), cout, st);
+                prep_kind = PREP_TAIL;
+                PB.M = M; PB.wG[p] = as<ScD>(B.wG); PB.wH[p] = as<ScD>(B.wH);
                 const size_t mm_ = M;
                 seg[nseg++] = {ms, Gh[p], M, L0};
                 seg[nseg++] = {ms + mm_, Hh[p], M, L0};
@@ -1635,7 +1643,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                 Z.h0 = h0;
                 Z.rGa = mont(rho_h[p][0][0]); Z.rGb = mont(rho_h[p][0][1]);
                 Z.rHa = mont(rho_h[p][0][2]); Z.rHb = mont(rho_h[p][0][3]);
-                launch_ipp_prep_lazy(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), cout, st);
+                prep_kind = PREP_LAZY;
+                PB.lz[p] = Z;
                 seg[nseg++] = {ms, at(Gm, h), h, L0, gn};
                 seg[nseg++] = {ms + hh, at(Gm, h + h0), h, L0, gn};
                 seg[nseg++] = {ms + 2 * hh, Hm, h, L0, gn};
@@ -1653,7 +1662,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                         Z.r0[v][c] = mont(rho_h[p][0][2 * v + c]);
                         Z.r1[v][c] = mont(rho_h[p][1][2 * v + c]);
                     }
-                launch_ipp_prep_deep2(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, Z, ms, as<ScD>(B.partial), cout, st);
+                prep_kind = PREP_DEEP2;
+                PB.dz[p] = Z;
                 for (int f = 0; f < 4; f++) {
                     const void *Bs = (f & 1) ? Hm : Gm;
                     const size_t x0 = (f == 0 || f == 3) ? hh : 0;
@@ -1662,7 +1672,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                                        (uint32_t)(f >> 1) + L0, gn};
                 }
             } else {
-                launch_ipp_prep(as<ScD>(B.a), as<ScD>(B.b), as<ScD>(B.yipm), A, ms, as<ScD>(B.partial), cout, st);
+                prep_kind = PREP_PLAIN;
                 // points whose a-scalar is zero (padding lanes) are left out of
                 // the job: L's G part runs over a_lo, R's over a_hi. In round
                 // 0 L's H part leaves out the padding lanes too: there
@@ -1677,6 +1687,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                 for (const MsmSeg &s : sl) if (s.count) seg[nseg++] = s;
             }
         }
+        launch_ipp_prep(PB, prep_kind, P, st);
         if (cur < 0)   // level-0 generator segments gather from the fixed-base tables
             for (int i = 0; i < nseg; i++) seg[i].wstride = gws;
         int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));

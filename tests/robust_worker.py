@@ -104,8 +104,9 @@ def stmts_hbm(foreign_gb):
     import workloads as W
     bpg = W._bpg()
     free, _ = torch.cuda.mem_get_info(0)
-    hog = torch.empty(int(min(foreign_gb * 1e9, free - 40e9)), dtype=torch.uint8, device="cuda:0")
+    hog = torch.empty(hog_bytes(foreign_gb, free), dtype=torch.uint8, device="cuda:0")
     torch.cuda.synchronize()
+    free_after, _ = torch.cuda.mem_get_info(0)
     texts = [W.config5(70000 + i) for i in range(24)]
     bpg.set_statements_layout(12, 4)
     err = None
@@ -118,7 +119,8 @@ def stmts_hbm(foreign_gb):
     ver = bool(outs) and outs[-1] is not None and bpg.verify("hbm", texts[-1][0], outs[-1][0], outs[-1][1], texts[-1][2])
     del hog
     print(json.dumps({"proved": sum(ok), "count": len(texts), "error": err, "last_error": bpg.last_error(),
-                      "stats": st, "verified_last": ver, "foreign_gb": round(hog_bytes(foreign_gb, free) / 1e9, 1)}),
+                      "stats": st, "verified_last": ver, "foreign_gb": round(hog_bytes(foreign_gb, free) / 1e9, 1),
+                      "free_gb_before": round(free / 1e9, 1), "free_gb_after_foreign": round(free_after / 1e9, 1)}),
           flush=True)
 
 
