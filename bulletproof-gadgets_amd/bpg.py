@@ -598,7 +598,7 @@ def last_batch_stats():
 
 STATEMENTS_STATS = ("workers", "consumers", "limit", "wall_ms", "synth_ms", "prepare_ms", "rng_ms", "prove_ms",
                     "worker_idle_ms", "consumer_idle_ms", "bound_stage", "hbm_limit", "est_gb_per_statement",
-                    "lockstep", "hbm_free_gb")
+                    "lockstep", "hbm_free_gb", "oom_retired")
 
 
 def last_statements_stats():
@@ -609,7 +609,7 @@ def last_statements_stats():
     d = dict(zip(STATEMENTS_STATS, arr))
     d["bound_stage"] = {0: "none", 1: "cpu workers (synthesis + prepare + rng)", 2: "device consumers"}.get(
         int(d["bound_stage"]), "?")
-    for k in ("workers", "consumers", "limit", "hbm_limit", "lockstep"):
+    for k in ("workers", "consumers", "limit", "hbm_limit", "lockstep", "oom_retired"):
         d[k] = int(d[k])
     wall = max(d["wall_ms"], 1e-9)
     d["worker_busy_frac"] = round(1 - d["worker_idle_ms"] / (wall * max(d["workers"], 1)), 3)

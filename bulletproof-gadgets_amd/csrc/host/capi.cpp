@@ -700,7 +700,7 @@ static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector
 namespace {
 std::atomic<uint32_t> g_stmt_consumers(0), g_stmt_lockstep(0);   // bpg_set_statements_layout (0: defaults)
 std::mutex g_ss_mu;
-double g_ss[15] = {0};   // bpg_last_statements_stats
+double g_ss[16] = {0};   // bpg_last_statements_stats
 }  // namespace
 int bpg_prove_statements(const char *name, const char *const *instances, const char *const *witnesses,
                          const char *const *gadgets, const uint64_t *seeds, uint32_t count, uint32_t threads,
@@ -746,6 +746,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         // RNG slot kept: no hipMalloc / hipFree per statement)
         std::vector<std::unique_ptr<PreparedCS>> spare;
         uint32_t next = 0, synth_busy = 0, inflight = 0, done = 0, proved = 0;
+        uint32_t consumers_left = 0, oom_retired = 0;   // device threads still proving; retired on OOM
         // statements in flight (synthesised, prepared, drawn or being proved):
         // a statement spends ~0.5 s between its synthesis and the end of its
         // RNG group's draw (the group forms from eight prepared statements),
@@ -891,6 +892,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                             c_fit = 1;
                         }
                         C_eff = c_fit;
+                        consumers_left = C_eff;
                         hbm_limit = (uint32_t)std::max<double>(std::min<double>(C_eff * L + 8, limit),
                                                                (all - C_eff * per_c) / est_st);
                         limit = std::min(limit, hbm_limit);
@@ -924,6 +926,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                 } else {
                     const auto t0 = std::chrono::steady_clock::now();
                     const int P = (int)items.size();
+                    bool oom = false;
                     try {
                         const PreparedCS *csv[MAX_LOCKSTEP];
                         const RngBlock *rbs[MAX_LOCKSTEP];
@@ -933,10 +936,37 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                         std::lock_guard<std::mutex> lk(mu);
                         proved += P;
                     } catch (const dev::HipError &e) {
-                        note_err(items[0]->k, std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr,
-                                 true);
+                        // a device thread whose workspace could not grow (the
+                        // admission's estimate was short): it hands its
+                        // statements back, frees its workspace and retires,
+                        // and the remaining device threads prove them (the
+                        // draws are on the device; proving is deterministic).
+                        // The last device thread does not retire: the error
+                        // ends the call.
+                        oom = e.err == hipErrorOutOfMemory;
+                        if (oom) {
+                            std::lock_guard<std::mutex> lk(mu);
+                            oom = consumers_left > 1;
+                            if (oom) consumers_left--;
+                        }
+                        if (!oom)
+                            note_err(items[0]->k,
+                                     std::string("HIP error: ") + hipGetErrorString(e.err) + " in " + e.expr, true);
                     } catch (const std::exception &e) {
                         note_err(items[0]->k, e.what(), false);
+                    }
+                    if (oom) {
+                        (void)hipGetLastError();
+                        try {
+                            release_thread_workspace(device);
+                        } catch (...) {
+                        }
+                        std::lock_guard<std::mutex> lk(mu);
+                        oom_retired++;
+                        for (auto it = items.rbegin(); it != items.rend(); ++it) ready.push_front(std::move(*it));
+                        items.clear();
+                        cv.notify_all();
+                        break;   // this device thread retires
                     }
                     const double ms = since_ms(t0);
                     std::lock_guard<std::mutex> lk(mu);
@@ -965,9 +995,9 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             const double wbusy = 1.0 - widle_ms / std::max(1e-9, wall * W);
             const double cbusy = 1.0 - cidle_ms / std::max(1e-9, wall * C_eff);
             const int bound = wbusy >= cbusy ? 1 : 2;
-            const double v[15] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
+            const double v[16] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
                                   widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9, (double)L,
-                                  adm_free_b / 1e9};
+                                  adm_free_b / 1e9, (double)oom_retired};
             std::lock_guard<std::mutex> lk(g_ss_mu);
             memcpy(g_ss, v, sizeof(v));
         }
@@ -992,7 +1022,7 @@ int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep) {
 }
 int bpg_last_statements_stats(double *out, int n) {
     std::lock_guard<std::mutex> lk(g_ss_mu);
-    for (int i = 0; i < n && i < 15; i++) out[i] = g_ss[i];
+    for (int i = 0; i < n && i < 16; i++) out[i] = g_ss[i];
     return 0;
 }
 

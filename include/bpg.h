@@ -93,7 +93,7 @@ int bpg_prove_statements(const char *name, const char *const *instances,
 int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep);
 
 /* Added: the last bpg_prove_statements of the process, per stage (ms summed
- * over threads; out[i], i < n <= 15): [0] CPU workers, [1] device consumers,
+ * over threads; out[i], i < n <= 16): [0] CPU workers, [1] device consumers,
  * [2] statements in flight allowed, [3] wall ms, [4] synthesis ms, [5]
  * prepare ms (transpose + upload + commitments), [6] TranscriptRng ms, [7]
  * device prove ms, [8] worker idle ms, [9] consumer idle ms, [10] the
@@ -102,9 +102,11 @@ int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep);
  * HBM admits (sized from the first prepared statement), [12] GB one prepared
  * statement holds, [13] statements a device thread proved at once (the
  * layout's lockstep, lowered when HBM does not hold one device thread of
- * that many), [14] free HBM (GB) when the admission was made. A call whose
- * free HBM does not hold one device thread of one statement fails before
- * proving with an error saying so (out[k] all NULL). (n <= 15) */
+ * that many), [14] free HBM (GB) when the admission was made, [15] device
+ * threads that retired because their workspace could not grow (their
+ * statements were proved by the others). A call whose free HBM does not hold
+ * one device thread of one statement fails before proving with an error
+ * saying so (out[k] all NULL). (n <= 16) */
 int bpg_last_statements_stats(double *out, int n);
 
 /* Added: `prover.num_constraints()` of the last c_prove on this thread

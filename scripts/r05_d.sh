@@ -15,4 +15,5 @@ LIBS="r05b:$PWD/bulletproof-gadgets_amd/variants/libbpg_r05b.so head:" bash scri
 db=$(find /tmp/${R}_prof -name '*.db' -print -quit)
 python3 scripts/prof_summary.py "$db" gpurun_out/${R}_profdefault_kernels.md > /dev/null || exit $?
 python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline_default.md 0.92 > /dev/null || exit $?
+timeout -k 10 180 bulletproof-gadgets_amd/bin/affine_bench > gpurun_out/${R}_affine_bench.txt 2>&1 || exit $?
 echo done
