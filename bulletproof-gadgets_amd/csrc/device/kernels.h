@@ -57,6 +57,8 @@ ProfSink *prof_sink();
 // (128 B, one line per random gather); folded generators are cached points
 // (160 B); MSM window rows returned to the host are extended.
 // out[i] = -in[i] (affine Niels: swap y+x / y-x, negate 2dxy)
+// out_i = G_i + H_i as cached points (count points; affine Niels inputs)
+void launch_gen_sum(const NielsD *G, const NielsD *H, PtD *out, uint32_t count, hipStream_t st);
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st);
 // out[i] = in[i] as affine Niels (cached in; one inversion per 32 points)
 // cached -> affine Niels for nvec <= 8 vectors of `count` points each, one launch
@@ -90,6 +92,9 @@ struct MsmSeg {
     // wstride + i (and its negation at + negofs); digits of all FB_W windows
     // go to one bucket row per MSM (0: an ordinary job)
     uint64_t wstride = 0;
+    // point indices of the segment's scalars (scal[k] multiplies base[idx[k]],
+    // idx[k] < 2^25); null: scal[k] multiplies base[k]
+    const uint32_t *idx = nullptr;
 };
 // Fixed-base generator tables (DESIGN.md "Fixed-base windows"): 20-bit
 // signed windows, 13 of them cover a canonical scalar.

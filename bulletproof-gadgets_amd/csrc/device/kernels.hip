@@ -241,6 +241,7 @@ struct SegTab {
     const void *neg[MSM_MAXSEG];    // negated copies (NEGC jobs), else = base
     uint32_t gofs[MSM_MAXSEG + 1];
     uint32_t row0[MSM_MAXSEG];
+    const uint32_t *idx[MSM_MAXSEG];   // point indices of the scalars (MsmSeg::idx), or null
     int n;
 };
 // val = sign << 31 | segment << 25 | point index within the segment: the
@@ -288,10 +289,15 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
     // argument struct would copy it to scratch
     __shared__ uint32_t gofs[MSM_MAXSEG + 1], srow0[MSM_MAXSEG];
     __shared__ const sc *sscal[MSM_MAXSEG];
+    __shared__ const uint32_t *sidx[MSM_MAXSEG];
     uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     if (threadIdx.x <= (uint32_t)T.n) gofs[threadIdx.x] = T.gofs[threadIdx.x];
-    if (threadIdx.x < (uint32_t)T.n) { srow0[threadIdx.x] = T.row0[threadIdx.x]; sscal[threadIdx.x] = T.scal[threadIdx.x]; }
+    if (threadIdx.x < (uint32_t)T.n) {
+        srow0[threadIdx.x] = T.row0[threadIdx.x];
+        sscal[threadIdx.x] = T.scal[threadIdx.x];
+        sidx[threadIdx.x] = T.idx[threadIdx.x];
+    }
     __syncthreads();
     for (uint64_t q = g; q < G.bflag_bytes / 16; q += stride) reinterpret_cast<uint4 *>(G.bflag)[q] = uint4{0, 0, 0, 0};
     if (G.tiles) {
@@ -321,7 +327,8 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
     sc_load(k, sscal[si] + (g - gofs[si]));
     uint32_t carry = 0, mask = (1u << c) - 1, full = 1u << c;
     const uint32_t m = srow0[si];
-    const uint32_t loc = (uint32_t)si << MSM_SEG_SHIFT | (g - gofs[si]);
+    const uint32_t *ix = sidx[si];
+    const uint32_t loc = (uint32_t)si << MSM_SEG_SHIFT | (ix ? ix[g - gofs[si]] : g - gofs[si]);
     for (int w = 0; w < W; w++) {
         int bit = w * c;
         int lo = bit >> 5, sh = bit & 31;
@@ -1080,6 +1087,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
                                   : segs[i].base;
         negc = negc && segs[i].negofs != 0;
         T.row0[i] = segs[i].msm;
+        T.idx[i] = segs[i].idx;
+        if (segs[i].idx && fb) throw HipError(hipErrorInvalidValue, "indexed fixed-base segment", __FILE__, __LINE__);
     }
     p.E0 = (uint64_t)Wd * total;
     p.T = RBK_T;
@@ -2781,6 +2790,24 @@ void launch_cached_to_niels(const PtD *const *in, NielsD *const *out, int nvec, 
     for (int v = 0; v < nvec; v++) { V.in[v] = AS_CGEC(in[v]); V.out[v] = AS_GEN(out[v]); }
     hipLaunchKernelGGL(k_cached_to_niels, dim3((count + CTN_B - 1) / CTN_B, (uint32_t)nvec), dim3(CTN_T), 0, st, V,
                        count);
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_gen_sum(const gen *__restrict__ G, const gen *__restrict__ H, gec *__restrict__ out, uint32_t count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    gen g, h;
+    gen_load(g, G + i);
+    gen_load(h, H + i);
+    ge a;
+    ge_from_niels(a, g);
+    ge_madd(a, a, h);
+    gec c;
+    ge_to_cached(c, a);
+    gec_store(out + i, c);
+}
+void launch_gen_sum(const NielsD *G, const NielsD *H, PtD *out, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_gen_sum, dim3(nblk(count, 64)), dim3(64), 0, st, AS_CGEN(G), AS_CGEN(H), AS_GEC(out), count);
     BPG_HIP(hipGetLastError());
 }
 void launch_niels_neg(const NielsD *in, NielsD *out, uint32_t count, hipStream_t st) {

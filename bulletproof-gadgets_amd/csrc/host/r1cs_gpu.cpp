@@ -108,6 +108,29 @@ GenSet::~GenSet() {
     if (G || H) (void)hipSetDevice(device);
     if (G) (void)hipFree(G);
     if (H) (void)hipFree(H);
+    if (GH) (void)hipFree(GH);
+}
+const dev::NielsD *gh_table(const GenSet &gs, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(gs.sums_mu);
+    if (gs.GH) return gs.GH;
+    BPG_HIP(hipSetDevice(gs.device));
+    dev::NielsD *gh = nullptr;
+    PtD *tmp = nullptr;
+    BPG_HIP(hipMalloc(&gh, 2 * (size_t)gs.N * sizeof(dev::NielsD)));
+    if (hipMalloc(&tmp, (size_t)gs.N * sizeof(PtD)) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(gh);
+        throw HipError(hipErrorOutOfMemory, "hipMalloc(G + H staging)", __FILE__, __LINE__);
+    }
+    launch_gen_sum(gs.G, gs.H, tmp, gs.N, st);
+    const PtD *in[1] = {tmp};
+    dev::NielsD *out[1] = {gh};
+    launch_cached_to_niels(in, out, 1, gs.N, st);
+    launch_niels_neg(gh, gh + gs.N, gs.N, st);
+    BPG_HIP(hipStreamSynchronize(st));
+    (void)hipFree(tmp);
+    gs.GH = gh;
+    return gh;
 }
 FbTables::~FbTables() {
     if (dev::process_exiting()) return;
@@ -671,7 +694,8 @@ PreparedCS::~PreparedCS() {
         memset(b, 0, host_slot_bytes);
         (void)hipHostFree(b);
     }
-    DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols};
+    DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols,
+                    &eqS, &eqI, &dfL, &dfR, &dfI};
     for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
 }
 
@@ -755,13 +779,34 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
     if (P->prover) {
         // a_L, a_R, a_O: this rank's lanes i = j * world + rank
         const uint32_t nl = P->nl;
-        std::vector<ScD> tmp(nl ? nl : 1);
+        std::vector<ScD> tmp(nl ? nl : 1), tL;
         const uint8_t *src[3] = {cs->a_L, cs->a_R, cs->a_O};
         DBuf *dst[3] = {&P->aL, &P->aR, &P->aO};
+        P->eq_split = false;
         for (int k = 0; k < 3; k++) {
             for (uint32_t j = 0; j < nl; j++)
                 tmp[j] = to_dev(Scalar::reduce(src[k] + 32 * ((size_t)j * world + rank)));
             up(*dst[k], tmp.data(), (size_t)nl * sizeof(ScD));
+            if (k == 0) tL = tmp;
+            if (k == 1 && world == 1) {
+                // lanes with a_L == a_R: one A_I1 term on G_i + H_i
+                std::vector<ScD> sE, sL, sR;
+                std::vector<uint32_t> iE, iD;
+                for (uint32_t j = 0; j < nl; j++) {
+                    if (!memcmp(&tL[j], &tmp[j], sizeof(ScD))) { iE.push_back(j); sE.push_back(tL[j]); }
+                    else { iD.push_back(j); sL.push_back(tL[j]); sR.push_back(tmp[j]); }
+                }
+                if (!iE.empty()) {
+                    P->eq_split = true;
+                    P->nE = (uint32_t)iE.size();
+                    P->nD = (uint32_t)iD.size();
+                    up(P->eqS, sE.data(), sE.size() * sizeof(ScD));
+                    up(P->eqI, iE.data(), iE.size() * 4);
+                    up(P->dfL, sL.data(), sL.size() * sizeof(ScD));
+                    up(P->dfR, sR.data(), sR.size() * sizeof(ScD));
+                    up(P->dfI, iD.data(), iD.size() * 4);
+                }
+            }
         }
         P->v.resize(m); P->vb.resize(m);
         std::vector<ScD> vbd(m ? m : 1);
@@ -788,7 +833,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
 size_t prepared_bytes(const PreparedCS &cs) {
     size_t b = 0;
     for (const DBuf *d : {&cs.aL, &cs.aR, &cs.aO, &cs.vb_dev, &cs.col_ptr, &cs.col_row, &cs.col_coeff, &cs.short_cols,
-                          &cs.long_cols})
+                          &cs.long_cols, &cs.eqS, &cs.eqI, &cs.dfL, &cs.dfR, &cs.dfI})
         b += d->cap;
     std::lock_guard<std::mutex> lk(cs.slot_mu);
     return b + cs.slot_bufs.size() * cs.slot_bytes;
@@ -1146,6 +1191,8 @@ void rng_draw_multi(const PreparedCS *const *cs, const uint8_t *label, size_t la
 // need no draw and start first, <s_L, G> starts once the s_L half of the
 // draws is on the device (streamed up in chunks as it is drawn) and only
 // <s_R, H> is left when the last draw is made.
+static void commit_a_segments(const PreparedCS &cp, const GenSet &gs, bool split_ok, const void *G0, const void *H0,
+                              int64_t gneg, uint64_t gws, hipStream_t st, MsmSeg *sg, int &ns);
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                const uint8_t entropy[32], ProveTimings *tm, const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
@@ -1166,11 +1213,12 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     const uint64_t gws = fbt ? 2 * (uint64_t)fbt->N : 0;
     PtD *rows = ws.rows_host, *rows_dev = ws.rows_view;
     if (nl) {
-        const MsmSeg sa[3] = {{as<ScD>(const_cast<DBuf &>(cs.aL)), G0, nl, 0, gneg, gws},
-                              {as<ScD>(const_cast<DBuf &>(cs.aR)), H0, nl, 0, gneg, gws},
-                              {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws}};
+        MsmSeg sa[4];
+        int ns = 0;
+        commit_a_segments(cs, *gs, !fbt, G0, H0, gneg, gws, ws.st, sa, ns);
+        sa[ns++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws};
         int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
-        pre.A = ws.msm->enqueue(sa, 3, 2, rows + CommitPre::ROWS_A, MSM_NIELS, rows_dev + CommitPre::ROWS_A);
+        pre.A = ws.msm->enqueue(sa, ns, 2, rows + CommitPre::ROWS_A, MSM_NIELS, rows_dev + CommitPre::ROWS_A);
         ws.prof_end(ph);
     }
     DrawProgress progress = [&](int v, hipEvent_t drawn) {
@@ -1252,6 +1300,27 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // batch, or distinct statements of one shape (n, m, N: the IPP and every
 // MSM job depend only on those; a_L/a_R/a_O, the constraint matrix and the
 // commitments are each proof's own).
+// A_I1's segments, <a_L, G> + <a_R, H> (MSM 0 of a commitment job): with the
+// prepared split (eq_split), lanes where a_L == a_R as ONE term a_L (G_i +
+// H_i) and the others as two (a quarter fewer entries when half the lanes
+// are equal, as in a MiMC circuit), else the plain two segments.
+static void commit_a_segments(const PreparedCS &cp, const GenSet &gs, bool split_ok, const void *G0, const void *H0,
+                              int64_t gneg, uint64_t gws, hipStream_t st, MsmSeg *sg, int &ns) {
+    const uint32_t nl = cp.nl;
+    if (cp.eq_split && split_ok && cp.world == 1) {
+        const dev::NielsD *GH = gh_table(gs, st);
+        if (cp.nE) sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.eqS)), GH, cp.nE, 0, gneg, 0,
+                               as<uint32_t>(const_cast<DBuf &>(cp.eqI))};
+        if (cp.nD) {
+            sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.dfL)), G0, cp.nD, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.dfI))};
+            sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.dfR)), H0, cp.nD, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.dfI))};
+        }
+        return;
+    }
+    sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.aL)), G0, nl, 0, gneg, gws};
+    sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.aR)), H0, nl, 0, gneg, gws};
+}
+
 // sum_{j in [a, b)} H_j of a generator set (one MSM with unit scalars on the
 // workspace's stream, once per range; rows land in the commitment half of the
 // pinned row buffer, which is free once the commitments are combined).
@@ -1340,8 +1409,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
     const size_t ROWS_PER_PROOF = 192;   // 3 MSMs x at most 64 windows
     MsmPlan pA[MAX_LOCKSTEP] = {};
     if (!pre) {
-        MsmSeg seg[5 * MAX_LOCKSTEP];
-        int nseg = 0;
+        MsmSeg seg[MAX_LOCKSTEP][6];
+        int nseg[MAX_LOCKSTEP] = {0};
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             const RngBlock &rb = *rbs[p];
@@ -1359,15 +1428,16 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             launch_wide_reduce(wd, nl, world, rank, as<ScD>(B.sL), st);
             launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(B.sR), st);
             const PreparedCS &cp = *csv[p];
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cp.aL)), G0, nl, 0, gneg, gws};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cp.aR)), H0, nl, 0, gneg, gws};
-            seg[nseg++] = {as<ScD>(const_cast<DBuf &>(cp.aO)), G0, nl, 1, gneg, gws};
-            seg[nseg++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
-            seg[nseg++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};
+            MsmSeg *sg = seg[p];
+            int &ns = nseg[p];
+            commit_a_segments(cp, *gs, !fbt, G0, H0, gneg, gws, st, sg, ns);
+            sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.aO)), G0, nl, 1, gneg, gws};
+            sg[ns++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
+            sg[ns++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};
         }
-        for (int p = 0; p < P && nseg; p++) {
+        for (int p = 0; p < P && nl; p++) {
             int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
-            pA[p] = ws.msm->enqueue(seg + 5 * p, 5, 3, rowsA + ROWS_PER_PROOF * p, MSM_NIELS,
+            pA[p] = ws.msm->enqueue(seg[p], nseg[p], 3, rowsA + ROWS_PER_PROOF * p, MSM_NIELS,
                                     rowsA_dev + ROWS_PER_PROOF * p);
             ws.prof_end(ph);
         }

@@ -40,6 +40,9 @@ struct GenSet {
     // round 0, gpu_prove_lockstep): computed once per range on first use
     mutable std::mutex sums_mu;
     mutable std::map<std::pair<uint32_t, uint32_t>, Point> h_sums;
+    // G_i + H_i (affine Niels, followed by their negations like G and H),
+    // built on first use (gh_table): A_I1's lanes with a_L == a_R
+    mutable dev::NielsD *GH = nullptr;
     ~GenSet();
 };
 // Comb tables of a generator set for the IPP's first two rounds:
@@ -127,6 +130,12 @@ struct PreparedCS {
     std::vector<uint8_t> V;             // m x 32 compressed commitments
     bool prover = true;
     DBuf aL, aR, aO, vb_dev;            // ScD arrays
+    // A_I1 = <a_L, G> + <a_R, H> as one term per lane on G_i + H_i where
+    // a_L_i == a_R_i (half the gates of a MiMC circuit: x + k squared) and two
+    // elsewhere (one rank only): compacted scalars and their lane indices
+    bool eq_split = false;
+    uint32_t nE = 0, nD = 0;
+    DBuf eqS, eqI, dfL, dfR, dfI;
     DBuf col_ptr, col_row, col_coeff, short_cols, long_cols;
     uint32_t nshort = 0, nlong = 0, ncol = 0;
     std::vector<uint32_t> huge_cols, col_ptr_host;
@@ -148,6 +157,9 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
                                        std::unique_ptr<PreparedCS> reuse = nullptr);
 // Device bytes a prepared statement holds (its arrays and RNG slots).
 size_t prepared_bytes(const PreparedCS &cs);
+// G_i + H_i of a full generator set (with negations at + gs.N), built on the
+// stream on first use and kept with the set.
+const dev::NielsD *gh_table(const GenSet &gs, hipStream_t st);
 
 // Per-thread workspace (stream + buffers), grown on demand.
 struct Workspace;
