@@ -1409,30 +1409,57 @@ DEVI void block_reduce_store(sc (&v)[K], sc *__restrict__ partial) {
         __syncthreads();
     }
 }
+// LDS tree over the block: on return thread 0's v[k] hold the block's sums
+template <int K>
+DEVI void block_reduce_lds(sc (&v)[K]) {
+    __shared__ sc sh[256];
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        sc_store(&sh[tid], v[k]);
+        for (int s = 128; s >= 1; s >>= 1) {
+            __syncthreads();
+            if (tid < (uint32_t)s) { sc a, b; sc_load(a, &sh[tid]); sc_load(b, &sh[tid + s]); sc_add(a, a, b); sc_store(&sh[tid], a); }
+        }
+        __syncthreads();
+        if (tid == 0) sc_load(v[k], &sh[0]);
+        __syncthreads();
+    }
+}
 #define RED_BLOCKS 1024
 // The launch's reduction ticket: a word after the partials (K <= 6 columns of
 // at most RED_BLOCKS blocks) of the caller's partial buffer, zeroed when the
 // buffer is allocated (grow_partial) and reset by each launch's last block.
 #define RED_TICKET RED_TICKET_WORD
-// Per-block partials (block_reduce_store), then the LAST block of the launch
-// to finish sums them column by column into out[k] (mode 0: Montgomery-
-// scaled partials, times R; 1: as is; 2: negated) -- one launch instead of
-// the kernel plus a k_reduce_cols launch. Hand-off per the agent-scope
-// release / acquire recipe (cdna_hip_programming.md Guideline 16, counter
-// form): every block's partial is drained and released before its ticket
-// add; the last block acquires before reading the other blocks' partials.
+// Per-block partials, then the LAST block of the launch to finish sums them
+// column by column into out[k] (mode 0: Montgomery-scaled partials, times R;
+// 1: as is; 2: negated) -- one launch instead of the kernel plus a
+// k_reduce_cols launch. Hand-off per cdna_hip_programming.md Guideline 16
+// (counter form, write-through variant): each block's partial is stored
+// sc1 (agent-scope relaxed atomic stores, written through to memory) and
+// drained before the block's relaxed ticket add, so no release fence (a
+// release writes back the whole L2 of the XCD, which the other streams'
+// kernels keep full of dirty lines); the last block acquires before reading
+// the partials.
 template <int K>
 DEVI void block_reduce_final(sc (&v)[K], sc *__restrict__ partial, sc *__restrict__ out, int mode) {
-    block_reduce_store<K>(v, partial);
+    block_reduce_lds<K>(v);   // thread 0 holds the block's sums
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            uint64_t *dst = reinterpret_cast<uint64_t *>(partial + blockIdx.x * K + k);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                __hip_atomic_store(dst + q, (uint64_t)v[k].v[2 * q] | (uint64_t)v[k].v[2 * q + 1] << 32,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     __shared__ sc sh[256];
     __shared__ uint32_t last;
     const uint32_t tid = threadIdx.x, nb = gridDim.x;
     uint32_t *ticket = reinterpret_cast<uint32_t *>(partial + RED_TICKET);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial's sc1 stores have landed
         const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = t == nb - 1 ? 1u : 0u;
         if (last) {
