@@ -1,24 +1,34 @@
 #!/bin/bash
-# End-of-round check B: the default bench command under rocprofv3
-# --kernel-trace --stats (kernel table + occupancy timeline; the bench's own
-# HIP-event bracketing on), the PMC passes of the current build (one counter
-# group per pass, kernel trace only), then the secondary modes, then the
-# --gpus launcher on hardware: two self-spawned ranks sharing the one GPU
-# over gloo (RCCL refuses two ranks on one device), config 4.
+# End-of-round records, two gpurun calls:
+#   R=<tag> bash scripts/final_check.sh prof    the default bench command under
+#       rocprofv3 --kernel-trace --stats (kernel table + occupancy timeline;
+#       the bench's own HIP-event bracketing on), then the PMC passes of the
+#       same build (one counter group per pass, kernel trace only) over the
+#       default layout at 48 proofs per step, reduced to a per-kernel table
+#       that pairs each kernel's HBM bytes with its algorithmic bytes from the
+#       same run
+#   R=<tag> bash scripts/final_check.sh modes   the driver's bench command, then
+#       the secondary modes (verify, verify-sharded, latency, statements) and
+#       the --gpus launcher with two self-spawned ranks sharing the one GPU
+#       over gloo (RCCL refuses two ranks on one device), config 4
 set -o pipefail
 mkdir -p gpurun_out
-R=${R:-r03z}
+R=${R:?tag}
 ROOTD=$(pwd)
-(cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/${R}_prof && \
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/${R}_prof -o run -- python3 $ROOTD/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $ROOTD/gpurun_out/${R}_profdefault_bench.json 2> $ROOTD/gpurun_out/${R}_profdefault.err) || exit $?
-db=$(find /tmp/${R}_prof -name '*.db' -print -quit)
-python3 scripts/prof_summary.py "$db" gpurun_out/${R}_profdefault_kernels.md > /dev/null || exit $?
-python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline_default.md 0.92 > /dev/null || exit $?
-R=${R} ARGS="--steps 1 --warmup 1 --threads 8 --batch 32 --no-cpu-baseline" bash scripts/pmc_passes.sh || exit $?
-python3 scripts/pmc_table.py gpurun_out/${R} gpurun_out/${R}_pmc.json > gpurun_out/${R}_pmc_table.md || exit $?
-timeout -k 10 300 python bench.py --mode verify --steps 3 --warmup 1 > gpurun_out/${R}_verify.json 2> gpurun_out/${R}_verify.err || exit $?
-timeout -k 10 300 python bench.py --mode verify-sharded --steps 20 --warmup 3 > gpurun_out/${R}_verify_sharded.json 2> gpurun_out/${R}_verify_sharded.err || exit $?
-timeout -k 10 300 python bench.py --mode latency --steps 5 --warmup 1 > gpurun_out/${R}_latency.json 2> gpurun_out/${R}_latency.err || exit $?
-timeout -k 10 600 python bench.py --mode statements --steps 2 --warmup 1 > gpurun_out/${R}_statements.json 2> gpurun_out/${R}_statements.err || exit $?
-BENCH_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --config 4 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${R}_bench_2ranks_shared_gpu.json 2> gpurun_out/${R}_bench_2ranks.err || exit $?
+if [ "$1" = prof ]; then
+  (cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/${R}_prof && \
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/${R}_prof -o run -- python3 $ROOTD/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $ROOTD/gpurun_out/${R}_profdefault_bench.json 2> $ROOTD/gpurun_out/${R}_profdefault.err) || exit $?
+  db=$(find /tmp/${R}_prof -name '*.db' -print -quit)
+  python3 scripts/prof_summary.py "$db" gpurun_out/${R}_profdefault_kernels.md > /dev/null || exit $?
+  python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline_default.md 0.92 > /dev/null || exit $?
+  R=${R} ARGS="--steps 1 --warmup 1 --batch 48 --no-cpu-baseline" bash scripts/pmc_passes.sh || exit $?
+  python3 scripts/pmc_table.py gpurun_out/${R} gpurun_out/${R}_pmc.json > gpurun_out/${R}_pmc_table.md || exit $?
+else
+  timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err || exit $?
+  timeout -k 10 300 python bench.py --mode verify --steps 3 --warmup 1 > gpurun_out/${R}_verify.json 2> gpurun_out/${R}_verify.err || exit $?
+  timeout -k 10 300 python bench.py --mode verify-sharded --steps 20 --warmup 3 > gpurun_out/${R}_verify_sharded.json 2> gpurun_out/${R}_verify_sharded.err || exit $?
+  timeout -k 10 300 python bench.py --mode latency --steps 5 --warmup 1 > gpurun_out/${R}_latency.json 2> gpurun_out/${R}_latency.err || exit $?
+  timeout -k 10 600 python bench.py --mode statements --steps 2 --warmup 1 > gpurun_out/${R}_statements.json 2> gpurun_out/${R}_statements.err || exit $?
+  BENCH_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --config 4 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${R}_bench_2ranks_shared_gpu.json 2> gpurun_out/${R}_bench_2ranks.err || exit $?
+fi
 echo done
