@@ -2688,20 +2688,23 @@ void launch_fb_build(const NielsD *gens, uint32_t N, NielsD *tab, hipStream_t st
     hipLaunchKernelGGL(k_fb_build, dim3(nblk(N, 64)), dim3(64), 0, st, AS_CGEN(gens), N, AS_GEN(tab));
     BPG_HIP(hipGetLastError());
 }
-// Cached points -> affine Niels with ONE field inversion per block of
-// CTN_T threads x CTN_K points (Montgomery's trick across the block): a
+// Cached points -> affine Niels with ONE field inversion per wave of 64
+// threads x CTN_K points (Montgomery's trick across the wave): a
 // materialised IPP level kept as Niels makes the MSM jobs over it 7M madds
 // at pass 1's three waves per SIMD, instead of 8M cached additions at two.
 // From (Y+X, Y-X, 2Z, 2dT): with zi = 2 / (2Z), y+x = (Y+X) zi, y-x =
 // (Y-X) zi, 2dxy = 2dT zi.
 // Each thread multiplies its CTN_K denominators (prefix products kept in
-// registers); the threads' products are scanned across the block -- wave
-// prefix and suffix products by lane shuffles, waves combined through LDS --
-// so that 1 / (thread product) = (1 / block product) x (product of the
-// threads before) x (product of the threads after); wave 0 inverts the block
-// product while the other waves wait. Per point about 9M + 265M / 1024, and
-// every lane busy (round 4's kernel ran one serial 32-point chain per thread:
-// 0.05 waves per SIMD, profiles/r04q_pmc_table.md).
+// registers); the lanes' products are scanned across the wave -- prefix and
+// suffix products by lane shuffles -- so that 1 / (lane product) =
+// (1 / wave product) x (product of the lanes before) x (product of the lanes
+// after); the whole wave inverts its product (the same issue slots one
+// lane's inversion would take, no barrier), then every thread walks back
+// through its four points. Per point about 9M + 204M / 256, every lane busy
+// (round 4's kernel ran one serial 32-point chain per thread: 0.05 waves per
+// SIMD, profiles/r04q_pmc_table.md; a block-wide version with one inversion
+// per 1,024 points kept three waves idle at a barrier while the fourth
+// inverted).
 static constexpr uint32_t CTN_T = 256, CTN_K = 4, CTN_B = CTN_T * CTN_K;
 DEVI void fe_load_g(fe &r, const uint32_t *w) {
 #pragma unroll
@@ -2732,9 +2735,7 @@ __global__ __launch_bounds__(CTN_T) void k_cached_to_niels(CtnArgs V, uint32_t c
     WAVE_PRIO(BPG_MISC_PRIO);
     const gec *__restrict__ in = V.in[blockIdx.y];
     gen *__restrict__ out = V.out[blockIdx.y];
-    __shared__ fe wprod[CTN_T / 64];   // each wave's product
-    __shared__ fe binv;                // 1 / block product
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t t = threadIdx.x, lane = t & 63;
     const uint64_t base = (uint64_t)blockIdx.x * CTN_B;
     constexpr int SW = sizeof(gec) / 4;
     // this thread's points: base + k CTN_T + t (coalesced across the block);
@@ -2765,29 +2766,20 @@ __global__ __launch_bounds__(CTN_T) void k_cached_to_niels(CtnArgs V, uint32_t c
         fe_mul(o, o, suf);
         if (lane + d < 64) suf = o;
     }
-    if (lane == 63) wprod[wv] = pre;
-    __syncthreads();
-    // products of the threads before (ex_pre) and after (ex_suf) this one
-    fe ex_pre, ex_suf;
+    // products of the lanes before (ex_pre) and after (ex_suf) this one;
+    // the wave's product (lane 63's prefix) is inverted by the whole wave:
+    // one inversion per 256 points costs every lane the same issue slots as
+    // one lane's would, and no wave waits at a barrier for another's
+    fe ex_pre, ex_suf, tot;
     fe_shfl_up(ex_pre, pre, 1);
     fe_shfl_down(ex_suf, suf, 1);
     if (lane == 0) fe_one(ex_pre);
     if (lane == 63) fe_one(ex_suf);
-    for (uint32_t j = 0; j < wv; j++) fe_mul(ex_pre, ex_pre, wprod[j]);
-    for (uint32_t j = wv + 1; j < CTN_T / 64; j++) fe_mul(ex_suf, ex_suf, wprod[j]);
-    if (wv == 0) {   // one wave inverts the block product
-        fe tot = wprod[0];
-        fe_in_vgprs(tot);
 #pragma unroll
-        for (uint32_t j = 1; j < CTN_T / 64; j++) fe_mul(tot, tot, wprod[j]);
-        fe inv;
-        fe_invert(inv, tot);
-        if (lane == 0) binv = inv;
-    }
-    __syncthreads();
-    fe inv, bi = binv;   // 1 / p
-    fe_in_vgprs(bi);
-    fe_mul(inv, bi, ex_pre);
+    for (int k = 0; k < 10; k++) tot.v[k] = (uint32_t)__shfl((int)pre.v[k], 63, 64);
+    fe inv;   // 1 / p
+    fe_invert(inv, tot);
+    fe_mul(inv, inv, ex_pre);
     fe_mul(inv, inv, ex_suf);
     // walk back through the thread's own points: 1 / (2Z_k) = inv_k q_(k-1),
     // inv_(k-1) = inv_k 2Z_k
