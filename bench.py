@@ -823,7 +823,7 @@ def bench_statements(a, bpg, dist, D, rank, world, W):
         if any(o is None for o in outs):
             raise SystemExit("bench: a statement failed: %s" % bpg.last_error())
         api = "bpg_prove_statements, %d CPU workers + %d device threads of up to %d statements" % (
-            threads, stages["consumers"] if stages else min(12 if a.consumers else 5, max(1, a.consumers or threads // 2)),
+            threads, stages["consumers"] if stages else min(a.consumers or 5, max(1, a.consumers or threads // 2)),
             a.stmt_lockstep or 4)
     if dist is not None:
         dt = D.max_over_ranks(dt)

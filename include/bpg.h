@@ -87,7 +87,8 @@ int bpg_prove_statements(const char *name, const char *const *instances,
                          struct ProofArtifacts **out);
 
 /* Added: layout of later bpg_prove_statements calls of the process: device
- * threads (1-12; 0, the default: min(5, threads / 2), fewer if HBM does not
+ * threads (1-64; 0, the default: min(5, threads / 2); each call takes at
+ * most one per hardware queue HIP gives the process, and fewer if HBM does not
  * hold them) and statements each proves at once (1-4; 0, the default: 4).
  * -1 if out of range. */
 int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep);
