@@ -2853,17 +2853,40 @@ void launch_from_mont(const ScD *src, uint32_t count, ScD *dst, hipStream_t st) 
 // verification_scalars): s_i = allinv * prod_{bit j of i} u_{lgn-1-j}^2.
 // w = flatten output [wL | wR | wO | ...]; u2m = Montgomery(u_k^2);
 // xm, am, bm, um Montgomery forms of x, ipp.a, ipp.b, r1cs u.
-__global__ void k_verify_gh(const sc *__restrict__ w, const sc *__restrict__ yipm, const sc *__restrict__ u2m,
-                            sc allinv, uint32_t n, uint32_t N, uint32_t lgn, sc xm, sc am, sc bm, sc um,
-                            sc *__restrict__ out, sc *__restrict__ ynwR) {
+// s_i = allinv * prod_{bit j of i} u_{lgn-1-j}^2 from two tables: tlo[k]
+// (Montgomery form) over the low `lo` bits of i, thi[k] (times allinv) over
+// the others, so s_i = thi[i >> lo] tlo[i mod 2^lo] is ONE product per
+// element instead of a product per bit of i (lgn of them; the low bits made
+// the lanes of a wave diverge, ~26 products per element at 2^20), and the
+// s for h, the complement bits, is s_(N-1-i) the same way.
+__global__ void k_verify_tables(const sc *__restrict__ u2m, uint32_t lgn, uint32_t lo, sc allinv,
+                                sc *__restrict__ tlo, sc *__restrict__ thi) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nlo = 1u << lo, nhi = 1u << (lgn - lo);
+    if (k < nlo) {
+        sc t, r2, one = sc_one_raw();
+        for (int q = 0; q < 8; q++) r2.v[q] = SC_R2[q];
+        mm(t, one, r2);   // 1 in Montgomery form (R mod l)
+        for (uint32_t j = 0; j < lo; j++)
+            if ((k >> j) & 1) { sc u; sc_load(u, u2m + (lgn - 1 - j)); mm(t, t, u); }
+        sc_store(tlo + k, t);
+    } else if (k - nlo < nhi) {
+        const uint32_t kk = k - nlo;
+        sc t = allinv;
+        for (uint32_t j = lo; j < lgn; j++)
+            if ((kk >> (j - lo)) & 1) { sc u; sc_load(u, u2m + (lgn - 1 - j)); mm(t, t, u); }
+        sc_store(thi + kk, t);
+    }
+}
+__global__ void k_verify_gh(const sc *__restrict__ w, const sc *__restrict__ yipm, const sc *__restrict__ tlo,
+                            const sc *__restrict__ thi, uint32_t lo, uint32_t n, uint32_t N, sc xm, sc am, sc bm,
+                            sc um, sc *__restrict__ out, sc *__restrict__ ynwR) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
-    sc si = allinv, sv = allinv, t;
-    for (uint32_t j = 0; j < lgn; j++) {
-        sc u; sc_load(u, u2m + (lgn - 1 - j));
-        if ((i >> j) & 1) mm(si, si, u);
-        else mm(sv, sv, u);          // bits of N-1-i are the complement of i's
-    }
+    const uint32_t mlo = (1u << lo) - 1, ic = N - 1 - i;
+    sc si, sv, p, q;
+    sc_load(p, thi + (i >> lo)); sc_load(q, tlo + (i & mlo)); mm(si, p, q);
+    sc_load(p, thi + (ic >> lo)); sc_load(q, tlo + (ic & mlo)); mm(sv, p, q);   // bits of N-1-i: the complement of i's
     sc yi; sc_load(yi, yipm + i);
     sc wL, wR, wO;
     if (i < n) { sc_load(wL, w + i); sc_load(wR, w + n + i); sc_load(wO, w + 2 * n + i); }
@@ -2881,14 +2904,16 @@ __global__ void k_verify_gh(const sc *__restrict__ w, const sc *__restrict__ yip
     if (i >= n) mm(h, h, um);
     sc_store(out + i, g);
     sc_store(out + N + i, h);
-    (void)t;
 }
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
-                      ScD xm, ScD am, ScD bm, ScD um, ScD *out, ScD *ynwR, hipStream_t st) {
-    hipLaunchKernelGGL(k_verify_gh, dim3(nblk(N, 128)), dim3(128), 0, st, AS_CSC(w), AS_CSC(yipm), AS_CSC(u2m),
-                       *reinterpret_cast<sc *>(&allinv), n, N, lgn, *reinterpret_cast<sc *>(&xm),
-                       *reinterpret_cast<sc *>(&am), *reinterpret_cast<sc *>(&bm), *reinterpret_cast<sc *>(&um),
-                       AS_SC(out), AS_SC(ynwR));
+                      ScD xm, ScD am, ScD bm, ScD um, ScD *tables, ScD *out, ScD *ynwR, hipStream_t st) {
+    const uint32_t lo = lgn < 10 ? lgn : 10, nlo = 1u << lo, nhi = 1u << (lgn - lo);
+    ScD *tlo = tables, *thi = tables + nlo;
+    hipLaunchKernelGGL(k_verify_tables, dim3(nblk(nlo + nhi, 128)), dim3(128), 0, st, AS_CSC(u2m), lgn, lo,
+                       *reinterpret_cast<sc *>(&allinv), AS_SC(tlo), AS_SC(thi));
+    hipLaunchKernelGGL(k_verify_gh, dim3(nblk(N, 128)), dim3(128), 0, st, AS_CSC(w), AS_CSC(yipm), AS_CSC(tlo),
+                       AS_CSC(thi), lo, n, N, *reinterpret_cast<sc *>(&xm), *reinterpret_cast<sc *>(&am),
+                       *reinterpret_cast<sc *>(&bm), *reinterpret_cast<sc *>(&um), AS_SC(out), AS_SC(ynwR));
     BPG_HIP(hipGetLastError());
 }
 

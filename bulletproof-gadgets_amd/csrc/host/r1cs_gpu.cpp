@@ -426,7 +426,7 @@ struct Workspace : dev::ProfSink {
     int device = 0;
     hipStream_t st = nullptr;
     std::unique_ptr<MsmEngine> msm;
-    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag, ghacc, vcomp, ones;
+    DBuf w, yipm, zlo, zhi, ylo, yhi, tabs, mscal, partial, small, gh, ynwR, pts, okflag, ghacc, vcomp, ones, vtab;
     PtD *rows_host = nullptr;        // pinned, 2 x ROWS_HALF window rows
     PtD *rows_view = nullptr;        // its device view (the row kernels write there)
     uint8_t *s_host = nullptr;       // pinned staging for s_L | s_R
@@ -447,7 +447,7 @@ struct Workspace : dev::ProfSink {
         if (s_host) (void)hipHostFree(s_host);
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&w, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs, &mscal, &partial, &small, &gh, &ynwR, &pts, &okflag,
-                        &ghacc, &vcomp, &ones};
+                        &ghacc, &vcomp, &ones, &vtab};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
         msm.reset();
         if (st) (void)hipStreamDestroy(st);
@@ -630,7 +630,7 @@ size_t thread_workspace_bytes(int device) {
 static size_t workspace_bytes(const Workspace &ws) {
     size_t b = ws.msm ? ws.msm->bytes() : 0;
     for (const DBuf *d : {&ws.w, &ws.yipm, &ws.zlo, &ws.zhi, &ws.ylo, &ws.yhi, &ws.tabs, &ws.mscal, &ws.partial,
-                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag, &ws.ghacc, &ws.vcomp, &ws.ones})
+                          &ws.small, &ws.gh, &ws.ynwR, &ws.pts, &ws.okflag, &ws.ghacc, &ws.vcomp, &ws.ones, &ws.vtab})
         b += d->cap;
     for (const ProofBufs &B : ws.pb)
         for (const DBuf *d : {&B.wide, &B.sL, &B.sR, &B.w, &B.wloc, &B.l1, &B.r0, &B.r1, &B.r3, &B.ypm, &B.yipm,
@@ -2152,8 +2152,10 @@ static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label
     ScD *u2d = as<ScD>(ws.small);
     if (lgn) BPG_HIP(hipMemcpyAsync(u2d, u2h, lgn * sizeof(ScD), hipMemcpyHostToDevice, st));
     ws.ynwR.grow((size_t)(n ? n : 1) * sizeof(ScD) + 64);
+    ws.vtab.grow((size_t)(2048 + 64) * sizeof(ScD));   // 2^min(lgn,10) + 2^(lgn-10) <= 2048 for lgn < 21
+    if (lgn > 20) ws.vtab.grow((size_t)((1u << 10) + (1u << (lgn - 10))) * sizeof(ScD));
     launch_verify_gh(as<ScD>(ws.w), as<ScD>(ws.yipm), u2d, to_dev(allinv), n, N, lgn, mont(x), mont(pa), mont(pb),
-                     mont(u), gh, as<ScD>(ws.ynwR), st);
+                     mont(u), as<ScD>(ws.vtab), gh, as<ScD>(ws.ynwR), st);
     grow_partial(ws.partial, st);
     ScD *dsm = u2d + 40;
     if (n) launch_dot(as<ScD>(ws.ynwR), as<ScD>(ws.w), n, as<ScD>(ws.partial), dsm, st);
