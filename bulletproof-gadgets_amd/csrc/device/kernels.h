@@ -298,9 +298,12 @@ void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq,
 void launch_ipp_tail_weights(ScD *const *wG, ScD *const *wH, const ScD (*r)[4], int P, uint32_t M, uint32_t h,
                              uint32_t n, hipStream_t st);
 // verifier helpers
-// the verifier's g / h scalars (tables: scratch of 2^min(lgn,10) + 2^(lgn-10) scalars)
+// the verifier's g / h scalars (tables: scratch of 2^min(lgn,10) + 2^(lgn-10)
+// scalars) into out[0..2N), or, with acc, added into acc weighted by rho
+// (written when first) if *ok (the proof's points decompressed)
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
-                      ScD xm, ScD am, ScD bm, ScD um, ScD *tables, ScD *out, ScD *ynwR, hipStream_t st);
+                      ScD xm, ScD am, ScD bm, ScD um, ScD *tables, ScD *out, ScD *ynwR, ScD *acc, ScD rho_mont,
+                      bool first, const int *ok, hipStream_t st);
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st);
 // sharded prover: dst[j] = src[j * stride + offset]
 void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st);

@@ -2880,7 +2880,8 @@ __global__ void k_verify_tables(const sc *__restrict__ u2m, uint32_t lgn, uint32
 }
 __global__ void k_verify_gh(const sc *__restrict__ w, const sc *__restrict__ yipm, const sc *__restrict__ tlo,
                             const sc *__restrict__ thi, uint32_t lo, uint32_t n, uint32_t N, sc xm, sc am, sc bm,
-                            sc um, sc *__restrict__ out, sc *__restrict__ ynwR) {
+                            sc um, sc *__restrict__ out, sc *__restrict__ ynwR, sc *__restrict__ acc, sc rhom,
+                            int first, const int *__restrict__ ok) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const uint32_t mlo = (1u << lo) - 1, ic = N - 1 - i;
@@ -2902,18 +2903,34 @@ __global__ void k_verify_gh(const sc *__restrict__ w, const sc *__restrict__ yip
     sc one = sc_one_raw();
     sc_sub(h, h, one);
     if (i >= n) mm(h, h, um);
-    sc_store(out + i, g);
-    sc_store(out + N + i, h);
+    if (!acc) {
+        sc_store(out + i, g);
+        sc_store(out + N + i, h);
+        return;
+    }
+    // batch verification: acc += rho (g, h), only for a proof whose points
+    // decompressed (the previous kernel on this stream set *ok)
+    if (!*ok) return;
+    mm(g, g, rhom);
+    mm(h, h, rhom);
+    if (!first) {
+        sc_load(a, acc + i); sc_add(g, g, a);
+        sc_load(a, acc + N + i); sc_add(h, h, a);
+    }
+    sc_store(acc + i, g);
+    sc_store(acc + N + i, h);
 }
 void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv, uint32_t n, uint32_t N, uint32_t lgn,
-                      ScD xm, ScD am, ScD bm, ScD um, ScD *tables, ScD *out, ScD *ynwR, hipStream_t st) {
+                      ScD xm, ScD am, ScD bm, ScD um, ScD *tables, ScD *out, ScD *ynwR, ScD *acc, ScD rho_mont,
+                      bool first, const int *ok, hipStream_t st) {
     const uint32_t lo = lgn < 10 ? lgn : 10, nlo = 1u << lo, nhi = 1u << (lgn - lo);
     ScD *tlo = tables, *thi = tables + nlo;
     hipLaunchKernelGGL(k_verify_tables, dim3(nblk(nlo + nhi, 128)), dim3(128), 0, st, AS_CSC(u2m), lgn, lo,
                        *reinterpret_cast<sc *>(&allinv), AS_SC(tlo), AS_SC(thi));
     hipLaunchKernelGGL(k_verify_gh, dim3(nblk(N, 128)), dim3(128), 0, st, AS_CSC(w), AS_CSC(yipm), AS_CSC(tlo),
                        AS_CSC(thi), lo, n, N, *reinterpret_cast<sc *>(&xm), *reinterpret_cast<sc *>(&am),
-                       *reinterpret_cast<sc *>(&bm), *reinterpret_cast<sc *>(&um), AS_SC(out), AS_SC(ynwR));
+                       *reinterpret_cast<sc *>(&bm), *reinterpret_cast<sc *>(&um), AS_SC(out), AS_SC(ynwR),
+                       AS_SC(acc), *reinterpret_cast<sc *>(&rho_mont), first ? 1 : 0, ok);
     BPG_HIP(hipGetLastError());
 }
 

@@ -2061,9 +2061,13 @@ struct VerifyTerms {
     std::vector<Scalar> ss;   // scalars of the small points
     Scalar sB, sBb;           // of B and B_blinding
 };
+// acc (batch verification): the g / h scalars weighted by rho are added into
+// acc (written when first) instead of stored in gh, on the device and only if
+// the proof's points decompressed (ok_dev)
 static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label_len, const uint8_t *V,
                         const uint8_t *proof, size_t plen, const uint8_t entropy[32], Workspace &ws, ScD *gh,
-                        NielsD *pts, int *ok_dev, int *ok_host, VerifyTerms &vt) {
+                        NielsD *pts, int *ok_dev, int *ok_host, VerifyTerms &vt, ScD *acc = nullptr,
+                        const Scalar *rho = nullptr, bool first = false) {
     const uint32_t n = cs.n, m = cs.m, N = cs.N;
     hipStream_t st = ws.st;
     // R1CSProof::from_bytes
@@ -2152,20 +2156,6 @@ static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label
     ScD *u2d = as<ScD>(ws.small);
     if (lgn) BPG_HIP(hipMemcpyAsync(u2d, u2h, lgn * sizeof(ScD), hipMemcpyHostToDevice, st));
     ws.ynwR.grow((size_t)(n ? n : 1) * sizeof(ScD) + 64);
-    ws.vtab.grow((size_t)(2048 + 64) * sizeof(ScD));   // 2^min(lgn,10) + 2^(lgn-10) <= 2048 for lgn < 21
-    if (lgn > 20) ws.vtab.grow((size_t)((1u << 10) + (1u << (lgn - 10))) * sizeof(ScD));
-    launch_verify_gh(as<ScD>(ws.w), as<ScD>(ws.yipm), u2d, to_dev(allinv), n, N, lgn, mont(x), mont(pa), mont(pb),
-                     mont(u), as<ScD>(ws.vtab), gh, as<ScD>(ws.ynwR), st);
-    grow_partial(ws.partial, st);
-    ScD *dsm = u2d + 40;
-    if (n) launch_dot(as<ScD>(ws.ynwR), as<ScD>(ws.w), n, as<ScD>(ws.partial), dsm, st);
-    else BPG_HIP(hipMemsetAsync(dsm, 0, sizeof(ScD), st));
-    // wV and wc back to the host
-    ScD *hsm = ws.small_host + 2100;
-    BPG_HIP(hipMemcpyAsync(hsm, dsm, sizeof(ScD), hipMemcpyDeviceToHost, st));
-    std::vector<ScD> wvh(m + 1);
-    BPG_HIP(hipMemcpyAsync(wvh.data(), as<ScD>(ws.w) + 3 * (size_t)n, (size_t)(m + 1) * sizeof(ScD),
-                           hipMemcpyDeviceToHost, st));
     // small points: A_I1, A_O1, S1, V_i, T_*, L_k, R_k
     const uint32_t ns = 3 + m + 5 + 2 * lgn;
     std::vector<uint8_t> comp((size_t)ns * 32);
@@ -2180,6 +2170,22 @@ static int verify_terms(const PreparedCS &cs, const uint8_t *label, size_t label
     uint32_t *compd = as<uint32_t>(ws.vcomp);
     BPG_HIP(hipMemcpyAsync(compd, comp.data(), comp.size(), hipMemcpyHostToDevice, st));
     launch_decompress(compd, pts, ok_dev, ns, st);
+    // g, h (after the decompression: a batch's accumulation is skipped on
+    // the device for a proof whose points do not decompress)
+    ws.vtab.grow((size_t)(2048 + 64) * sizeof(ScD));   // 2^min(lgn,10) + 2^(lgn-10) <= 2048 for lgn < 21
+    if (lgn > 20) ws.vtab.grow((size_t)((1u << 10) + (1u << (lgn - 10))) * sizeof(ScD));
+    launch_verify_gh(as<ScD>(ws.w), as<ScD>(ws.yipm), u2d, to_dev(allinv), n, N, lgn, mont(x), mont(pa), mont(pb),
+                     mont(u), as<ScD>(ws.vtab), gh, as<ScD>(ws.ynwR), acc, rho ? mont(*rho) : ScD{}, first, ok_dev, st);
+    grow_partial(ws.partial, st);
+    ScD *dsm = u2d + 40;
+    if (n) launch_dot(as<ScD>(ws.ynwR), as<ScD>(ws.w), n, as<ScD>(ws.partial), dsm, st);
+    else BPG_HIP(hipMemsetAsync(dsm, 0, sizeof(ScD), st));
+    // wV and wc back to the host
+    ScD *hsm = ws.small_host + 2100;
+    BPG_HIP(hipMemcpyAsync(hsm, dsm, sizeof(ScD), hipMemcpyDeviceToHost, st));
+    std::vector<ScD> wvh(m + 1);
+    BPG_HIP(hipMemcpyAsync(wvh.data(), as<ScD>(ws.w) + 3 * (size_t)n, (size_t)(m + 1) * sizeof(ScD),
+                           hipMemcpyDeviceToHost, st));
     BPG_HIP(hipMemcpyAsync(ok_host, ok_dev, 4, hipMemcpyDeviceToHost, st));
     ws.sync();
     Scalar delta = from_dev(hsm[0]);
@@ -2302,9 +2308,10 @@ static void verify_batch_set(const PreparedCS &cs, const uint8_t *label, size_t 
         BPG_HIP(hipMemcpyAsync(ws.okflag.p, &one, 4, hipMemcpyHostToDevice, st));
         VerifyTerms vt;
         if (!verify_terms(cs, label, label_len, V, proofs + stride * (size_t)j, lens[j], entropy, ws,
-                          as<ScD>(ws.gh), as<NielsD>(ws.pts) + off, as<int>(ws.okflag), &ok, vt) || !ok)
-            continue;   // rejected on its own
-        launch_sc_axpy(as<ScD>(ws.ghacc), as<ScD>(ws.gh), 2 * N, mont(rho), first, st);
+                          as<ScD>(ws.gh), as<NielsD>(ws.pts) + off, as<int>(ws.okflag), &ok, vt, as<ScD>(ws.ghacc),
+                          &rho, first) ||
+            !ok)
+            continue;   // rejected on its own (its g / h were not accumulated)
         first = false;
         for (uint32_t i = 0; i < vt.ns; i++) ss_all.push_back(vt.ss[i] * rho);
         sB = sB + vt.sB * rho;
