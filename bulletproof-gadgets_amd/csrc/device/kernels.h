@@ -195,7 +195,6 @@ struct IppRoundArgs {
 // c_R -> msm_scal[4h+1]
 // c_out: c_L, c_R (2 scalars; may be a device view of pinned host memory)
 // acc = (first ? 0 : acc) + x * rho mod l (rho in Montgomery form)
-void launch_sc_axpy(ScD *acc, const ScD *x, uint32_t count, ScD rho_mont, bool first, hipStream_t st);
 // a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u (Montgomery u, u^-1) for
 // the P <= 4 proofs of a lockstep step in one launch
 void launch_ipp_fold_scalars(ScD *const *a, ScD *const *b, const ScD *u, const ScD *uinv, int P, uint32_t h,

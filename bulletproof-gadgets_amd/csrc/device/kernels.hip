@@ -1633,25 +1633,6 @@ __global__ void k_ipp_fold_scalars(FoldScalarsArgs A, uint32_t h) {
     sc_load(x, a + i); sc_load(y, a + h + i); mm(t1, x, um); mm(t2, y, uim); sc_add(t1, t1, t2); sc_store(a + i, t1);
     sc_load(x, b + i); sc_load(y, b + h + i); mm(t1, x, uim); mm(t2, y, um); sc_add(t1, t1, t2); sc_store(b + i, t1);
 }
-// acc = (first ? 0 : acc) + x * rho mod l (x, acc canonical; rho in
-// Montgomery form): the batch verifier's weighted sum of the proofs'
-// generator scalars
-__global__ void k_sc_axpy(sc *__restrict__ acc, const sc *__restrict__ x, uint32_t count, sc rho, int first) {
-    WAVE_PRIO(BPG_MISC_PRIO);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    sc v, t;
-    sc_load(v, x + i);
-    mm(t, v, rho);
-    if (!first) { sc_load(v, acc + i); sc_add(t, t, v); }
-    sc_store(acc + i, t);
-}
-void launch_sc_axpy(ScD *acc, const ScD *x, uint32_t count, ScD rho_mont, bool first, hipStream_t st) {
-    if (!count) return;
-    hipLaunchKernelGGL(k_sc_axpy, dim3(nblk(count, 256)), dim3(256), 0, st, AS_SC(acc), AS_CSC(x), count,
-                       *reinterpret_cast<sc *>(&rho_mont), first ? 1 : 0);
-    BPG_HIP(hipGetLastError());
-}
 void launch_ipp_fold_scalars(ScD *const *a, ScD *const *b, const ScD *u, const ScD *uinv, int P, uint32_t h,
                              hipStream_t st) {
     if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "fold scalars proofs", __FILE__, __LINE__);

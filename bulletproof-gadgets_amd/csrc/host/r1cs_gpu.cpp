@@ -2283,8 +2283,7 @@ static void verify_batch_set(const PreparedCS &cs, const uint8_t *label, size_t 
     hipStream_t st = ws.st;
     const uint32_t ns_max = 3 + cs.m + 5 + 2 * 32;
     const uint32_t count = (uint32_t)idx.size();
-    ws.gh.grow((size_t)2 * N * sizeof(ScD) + 64);
-    ws.ghacc.grow((size_t)2 * N * sizeof(ScD) + 64);
+    ws.ghacc.grow((size_t)2 * N * sizeof(ScD) + 64);   // (verify_terms accumulates, gh is not written)
     ws.pts.grow(2 * (size_t)count * ns_max * sizeof(NielsD) + 64);
     ws.okflag.grow(64);
     // the weights: bound to every proof and to entropy the prover cannot know
