@@ -144,7 +144,7 @@ class MsmEngine {
     void reserve(const MsmPlan &p);
     hipStream_t st_;
     DBuf keys_, vals_, keys2_, vals2_, sort_tmp_, rk_a_, rk_b_, rp_a_, rp_b_, buckets_,
-        bflag_, segacc_, rows_dev_, tiles_;
+        bflag_, segacc_, rows_dev_, tiles_, dhist_;
     uint32_t *tiles_host_ = nullptr;     // pinned staging of the sort tile table
     hipEvent_t tiles_ev_ = nullptr;      // its upload has completed
 };

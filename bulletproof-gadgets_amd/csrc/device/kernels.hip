@@ -281,6 +281,12 @@ struct TileGeo {
     uint8_t *bflag;                   // cleared: bflag_bytes (multiple of 16)
     uint64_t bflag_bytes;
     uint32_t *tiles;                  // null: the host wrote the table
+    // the sort's first-pass histogram, counted here (null: k_rs_hist counts
+    // it): block = (point tile b, part s of S); hist[d nt + w TW + b] for
+    // digit d = key & (hbins - 1); parts of a tile hand their counts to the
+    // tile's last part through hpart / htick (S > 1)
+    uint32_t *hist, *hpart, *htick;
+    uint32_t hbins, S, sub;           // bins; parts per tile; points per part
 };
 __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nmsm, uint32_t half,
                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, TileGeo G, uint32_t wstride) {
@@ -321,7 +327,9 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
             }
         }
     }
-    if (g >= total) return;
+    extern __shared__ uint32_t lh[];   // fused histogram: [w][hbins]
+    const uint32_t hmask = G.hbins - 1;
+    auto point = [&](uint32_t g, bool count) {
     int si = seg_of(gofs, T.n, g);
     sc k;
     sc_load(k, sscal[si] + (g - gofs[si]));
@@ -358,9 +366,59 @@ __global__ void k_msm_digits(SegTab T, uint32_t total, int c, int W, uint32_t nm
         // [m][w][point of m]
         const size_t pos = wstride ? (size_t)W * G.pmoff[m] + (size_t)w * G.pmtot[m] + (g - G.pmoff[m])
                                    : (size_t)w * total + g;
-        keys[pos] = row << c | slot;
+        const uint32_t key = row << c | slot;
+        keys[pos] = key;
         vals[pos] = val;
+        if (count) atomicAdd(&lh[w * G.hbins + (key & hmask)], 1u);
     }
+    };
+    if (!G.hist) {
+        if (g < total) point(g, false);
+        return;
+    }
+    // fused first-pass histogram (window-major jobs with a device tile table)
+    const uint32_t nw = (uint32_t)W * G.hbins, tid = threadIdx.x;
+    for (uint32_t i = tid; i < nw; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+    const uint32_t b = blockIdx.x / G.S, part = blockIdx.x % G.S;
+    uint32_t mm_ = 0;
+    while (mm_ + 1 < nmsm && b >= G.cum[mm_ + 1]) mm_++;
+    const uint32_t j = b - G.cum[mm_];
+    const uint32_t p1 = G.moff[mm_] + min(G.mtot[mm_], (j + 1) * G.tile);
+    const uint32_t q0 = G.moff[mm_] + j * G.tile + part * G.sub, q1 = min(p1, q0 + G.sub);
+    for (uint32_t q = q0 + tid; q < q1; q += blockDim.x) point(q, true);
+    __syncthreads();
+    if (G.S == 1) {
+        for (uint32_t i = tid; i < nw; i += blockDim.x)
+            G.hist[(size_t)(i & hmask) * G.nt + (i / G.hbins) * G.TW + b] = lh[i];
+        return;
+    }
+    // hand-off to the tile's last part: written-through partial stores
+    // drained before the ticket add (as block_reduce_final)
+    uint32_t *mine = G.hpart + (size_t)blockIdx.x * nw;
+    for (uint32_t i = tid; i < nw; i += blockDim.x)
+        __hip_atomic_store(mine + i, lh[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(G.htick + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == G.S - 1 ? 1u : 0u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    const uint32_t *parts = G.hpart + (size_t)b * G.S * nw;
+    for (uint32_t i = tid; i < nw; i += blockDim.x) {
+        uint32_t v = lh[i];
+        for (uint32_t s2 = 0; s2 < G.S; s2++)
+            if (s2 != part) v += parts[(size_t)s2 * nw + i];
+        G.hist[(size_t)(i & hmask) * G.nt + (i / G.hbins) * G.TW + b] = v;
+    }
+    if (tid == 0) __hip_atomic_store(G.htick + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next job
 }
 
 // ---------------------------------------------------------------------------
@@ -392,28 +450,48 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict
     if (threadIdx.x < RS_BINS) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 // per digit d (one block each): exclusive scan of hist[d][0..nb) in place,
-// total[d] = the digit's count
+// total[d] = the digit's count. 2048 counts per step: 8 consecutive per
+// thread summed serially, the threads' sums scanned by wave shuffles, the
+// four waves' totals through LDS (two barriers per step).
+#define RS_SCAN_K 8
 __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ total) {
-    __shared__ uint32_t sm[256];
+    __shared__ uint32_t wsum[4];
     WAVE_PRIO(BPG_SORT_PRIO);
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint32_t *h = hist + (size_t)blockIdx.x * nb;
     uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < nb; r0 += 256) {
-        const uint32_t i = r0 + t;
-        const uint32_t v = i < nb ? h[i] : 0u;
-        sm[t] = v;
-        __syncthreads();
-        for (uint32_t d = 1; d < 256; d <<= 1) {
-            const uint32_t a = t >= d ? sm[t - d] : 0u;
-            __syncthreads();
-            sm[t] += a;
-            __syncthreads();
+    for (uint32_t r0 = 0; r0 < nb; r0 += 256 * RS_SCAN_K) {
+        const uint32_t i0 = r0 + t * RS_SCAN_K;
+        uint32_t v[RS_SCAN_K], sum = 0;
+#pragma unroll
+        for (int k = 0; k < RS_SCAN_K; k++) {
+            v[k] = i0 + k < nb ? h[i0 + k] : 0u;
+            sum += v[k];
         }
-        if (i < nb) h[i] = carry + sm[t] - v;
-        carry += sm[255];
+        uint32_t x = sum;   // inclusive scan over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            x += lane >= (uint32_t)d ? y : 0u;
+        }
+        if (lane == 63) wsum[wave] = x;
         __syncthreads();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t ws = wsum[q];
+            before += q < wave ? ws : 0u;
+            all += ws;
+        }
+        uint32_t run = carry + before + x - sum;
+#pragma unroll
+        for (int k = 0; k < RS_SCAN_K; k++) {
+            if (i0 + k < nb) h[i0 + k] = run;
+            run += v[k];
+        }
+        carry += all;
+        __syncthreads();   // wsum is rewritten by the next step
     }
     if (t == 0) total[blockIdx.x] = carry;
 }
@@ -945,7 +1023,7 @@ MsmEngine::~MsmEngine() {
     if (tiles_ev_) (void)hipEventDestroy(tiles_ev_);
     if (tiles_host_) (void)hipHostFree(tiles_host_);
     DBuf *bufs[] = {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_,
-                    &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &bflag_, &segacc_, &rows_dev_};
+                    &rk_a_, &rk_b_, &rp_a_, &rp_b_, &buckets_, &bflag_, &segacc_, &rows_dev_, &dhist_};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
 }
@@ -966,10 +1044,15 @@ void DBuf::grow(size_t need) {
 }
 
 static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::grow's allocation
+// the digit launch's histogram hand-off: RS_MAXTILES tickets, then at most
+// DHIST_PARTS parts' counts of 256 bins
+#define DHIST_PARTS 16384
+#define DHIST_BYTES ((size_t)(RS_MAXTILES + (size_t)DHIST_PARTS * RS_MAXBINS) * 4)
+#define DIG_LDS_WORDS 8192   // fused histogram in LDS: windows x bins
 size_t MsmEngine::bytes() const {
     size_t b = 0;
     for (const DBuf *d : {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_, &rk_a_, &rk_b_, &rp_a_, &rp_b_,
-                          &buckets_, &bflag_, &segacc_, &rows_dev_})
+                          &buckets_, &bflag_, &segacc_, &rows_dev_, &dhist_})
         b += d->cap;
     return b;
 }
@@ -982,7 +1065,7 @@ size_t MsmEngine::job_bytes(uint64_t total, int nmsm, int fmt) {
     return 4 * grown(E0 * 4) + grown((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256) + grown((size_t)6 * RS_MAXTILES * 4) +
            grown(capE * 4) + grown(capE * sizeof(ge)) + grown(capE + 1024) + grown((capE / 4 + 256) * sizeof(ge)) +
            grown(rows * half * sizeof(ge)) + grown(rows * half) + grown(2 * rows * nseg * sizeof(ge)) +
-           grown(rows * sizeof(ge));
+           grown(rows * sizeof(ge)) + grown(DHIST_BYTES);
 }
 void MsmEngine::reserve(const MsmPlan &p) {
     size_t kb = p.E0 * 4;
@@ -1000,18 +1083,22 @@ void MsmEngine::reserve(const MsmPlan &p) {
 // Sort (keys, vals) by the low key_bits within each row (tiles never straddle
 // a row; tiles_dev: nt x {start, end, first tile of the row, one past its last
 // tile, row start}); swaps the buffer pointers to the sorted pair.
+// 8-bit digits only where they save a pass (their scatter costs more LDS)
+static int rs_bits(int key_bits) { return (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7; }
+// first_counted: the digit launch already wrote the first pass's histogram
 static void radix_sort(uint32_t *&k, uint32_t *&v, uint32_t *&k2, uint32_t *&v2, int key_bits, const uint32_t *tiles,
-                       uint32_t nt, uint32_t *hist, hipStream_t st) {
+                       uint32_t nt, uint32_t *hist, bool first_counted, hipStream_t st) {
     if (!nt || key_bits < 1) return;
-    // 8-bit digits only where they save a pass (their scatter costs more LDS)
-    const int bits = (key_bits + 7) / 8 < (key_bits + 6) / 7 ? 8 : 7;
+    const int bits = rs_bits(key_bits);
     const uint32_t bins = 1u << bits;
     uint32_t *total = hist + (size_t)bins * nt;
     for (int shift = 0; shift < key_bits; shift += bits) {
         // every pass after the first keeps the order of equal digits (the
         // three-pass sorts of 20-bit fixed-base keys need the middle one too)
         const bool stable = shift > 0;
-        if (bits == 8)
+        if (shift == 0 && first_counted)
+            ;
+        else if (bits == 8)
             hipLaunchKernelGGL(k_rs_hist<8>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
         else
             hipLaunchKernelGGL(k_rs_hist<7>, dim3(nt), dim3(RS_BLOCK), 0, st, k, shift, tiles, nt, hist);
@@ -1172,10 +1259,34 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     }
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     ge *buckets = AS_GE(buckets_.p);
-    hipLaunchKernelGGL(k_msm_digits, dim3(nblk(total, 256)), dim3(256), 0, st_, T, (uint32_t)total, p.c, Wd,
+    // the first sort pass's histogram in the digit launch: one block per
+    // part of a tile of points (S parts, >= ~2048 blocks in all), each
+    // counting its W windows' keys in LDS
+    const uint32_t hbins = 1u << rs_bits((int)p.key_bits);
+    const bool fused = geo.tiles && !fb && (uint64_t)Wd * hbins <= DIG_LDS_WORDS;
+    uint32_t nblocks = nblk(total, 256);
+    size_t lds = 0;
+    if (fused) {
+        if (!dhist_.p) {
+            dhist_.grow(DHIST_BYTES);
+            BPG_HIP(hipMemsetAsync(dhist_.p, 0, (size_t)RS_MAXTILES * 4, st_));   // tickets
+        }
+        uint32_t S = std::min<uint32_t>(16, std::max<uint32_t>(1, (2048 + geo.TW - 1) / geo.TW));
+        while (S > 1 && (uint64_t)geo.TW * S * Wd > DHIST_PARTS) S--;
+        geo.hist = (uint32_t *)sort_tmp_.p;
+        geo.htick = (uint32_t *)dhist_.p;
+        geo.hpart = geo.htick + RS_MAXTILES;
+        geo.hbins = hbins;
+        geo.S = S;
+        geo.sub = (uint32_t)((tile + S - 1) / S + 63) / 64 * 64;
+        nblocks = geo.TW * S;
+        lds = (size_t)Wd * hbins * 4;
+    }
+    hipLaunchKernelGGL(k_msm_digits, dim3(nblocks), dim3(256), lds, st_, T, (uint32_t)total, p.c, Wd,
                        (uint32_t)nmsm, (uint32_t)p.half, keys, vals, geo, (uint32_t)wstride);
     BPG_HIP(hipGetLastError());
-    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p, st_);
+    radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p,
+               fused, st_);
     // reduce passes: E shrinks 8x per pass (2 slots per 16 entries)
     uint64_t E = p.E0;
     const uint32_t *kin = keys;
