@@ -306,6 +306,8 @@ void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv,
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st);
 // sharded prover: dst[j] = src[j * stride + offset]
 void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st);
+// dst[j] = src[idx[j]], j < count
+void launch_gather_idx(const ScD *src, const uint32_t *idx, uint32_t count, ScD *dst, hipStream_t st);
 void launch_gather_niels(const NielsD *src, uint32_t count, uint32_t stride, uint32_t offset, NielsD *dst,
                          hipStream_t st);
 // Montgomery -> canonical

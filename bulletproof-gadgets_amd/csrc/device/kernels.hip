@@ -450,48 +450,48 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict
     if (threadIdx.x < RS_BINS) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 // per digit d (one block each): exclusive scan of hist[d][0..nb) in place,
-// total[d] = the digit's count. 2048 counts per step: 8 consecutive per
-// thread summed serially, the threads' sums scanned by wave shuffles, the
-// four waves' totals through LDS (two barriers per step).
+// total[d] = the digit's count. 2048 counts per step, loaded up front
+// (coalesced, 8 per thread), then scanned 256 at a time: wave shuffles inside
+// each wave, the four waves' totals through LDS (double-buffered: one barrier
+// per 256 counts).
 #define RS_SCAN_K 8
 __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ total) {
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[2][4];
     WAVE_PRIO(BPG_SORT_PRIO);
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint32_t *h = hist + (size_t)blockIdx.x * nb;
-    uint32_t carry = 0;
+    uint32_t carry = 0, par = 0;
     for (uint32_t r0 = 0; r0 < nb; r0 += 256 * RS_SCAN_K) {
-        const uint32_t i0 = r0 + t * RS_SCAN_K;
-        uint32_t v[RS_SCAN_K], sum = 0;
+        uint32_t v[RS_SCAN_K];
 #pragma unroll
         for (int k = 0; k < RS_SCAN_K; k++) {
-            v[k] = i0 + k < nb ? h[i0 + k] : 0u;
-            sum += v[k];
+            const uint32_t i = r0 + k * 256 + t;
+            v[k] = i < nb ? h[i] : 0u;
         }
-        uint32_t x = sum;   // inclusive scan over the wave
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            x += lane >= (uint32_t)d ? y : 0u;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t ws = wsum[q];
-            before += q < wave ? ws : 0u;
-            all += ws;
-        }
-        uint32_t run = carry + before + x - sum;
 #pragma unroll
         for (int k = 0; k < RS_SCAN_K; k++) {
-            if (i0 + k < nb) h[i0 + k] = run;
-            run += v[k];
+            if (r0 + k * 256 >= nb) break;   // uniform
+            uint32_t x = v[k];   // inclusive scan over the wave
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                x += lane >= (uint32_t)d ? y : 0u;
+            }
+            if (lane == 63) wsum[par][wave] = x;
+            __syncthreads();
+            uint32_t before = 0, all = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t ws = wsum[par][q];
+                before += q < wave ? ws : 0u;
+                all += ws;
+            }
+            const uint32_t i = r0 + k * 256 + t;
+            if (i < nb) h[i] = carry + before + x - v[k];
+            carry += all;
+            par ^= 1u;
         }
-        carry += all;
-        __syncthreads();   // wsum is rewritten by the next step
     }
     if (t == 0) total[blockIdx.x] = carry;
 }
@@ -1049,6 +1049,10 @@ static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::gr
 #define DHIST_PARTS 16384
 #define DHIST_BYTES ((size_t)(RS_MAXTILES + (size_t)DHIST_PARTS * RS_MAXBINS) * 4)
 #define DIG_LDS_WORDS 8192   // fused histogram in LDS: windows x bins
+// fused launch: 1024-thread blocks (fewer parts per tile for the same
+// threads, so less hand-off traffic and a shorter last-part sum), ~512 blocks
+#define DIG_FUSED_THREADS 1024
+#define DIG_FUSED_BLOCKS 512
 size_t MsmEngine::bytes() const {
     size_t b = 0;
     for (const DBuf *d : {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_, &rk_a_, &rk_b_, &rp_a_, &rp_b_,
@@ -1260,8 +1264,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     ge *buckets = AS_GE(buckets_.p);
     // the first sort pass's histogram in the digit launch: one block per
-    // part of a tile of points (S parts, >= ~2048 blocks in all), each
-    // counting its W windows' keys in LDS
+    // part of a tile of points (S parts, ~512 blocks of 1024 threads in
+    // all), each counting its W windows' keys in LDS
     const uint32_t hbins = 1u << rs_bits((int)p.key_bits);
     const bool fused = geo.tiles && !fb && (uint64_t)Wd * hbins <= DIG_LDS_WORDS;
     uint32_t nblocks = nblk(total, 256);
@@ -1271,18 +1275,18 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
             dhist_.grow(DHIST_BYTES);
             BPG_HIP(hipMemsetAsync(dhist_.p, 0, (size_t)RS_MAXTILES * 4, st_));   // tickets
         }
-        uint32_t S = std::min<uint32_t>(16, std::max<uint32_t>(1, (2048 + geo.TW - 1) / geo.TW));
+        uint32_t S = std::min<uint32_t>(16, std::max<uint32_t>(1, (DIG_FUSED_BLOCKS + geo.TW - 1) / geo.TW));
         while (S > 1 && (uint64_t)geo.TW * S * Wd > DHIST_PARTS) S--;
         geo.hist = (uint32_t *)sort_tmp_.p;
         geo.htick = (uint32_t *)dhist_.p;
         geo.hpart = geo.htick + RS_MAXTILES;
         geo.hbins = hbins;
         geo.S = S;
-        geo.sub = (uint32_t)((tile + S - 1) / S + 63) / 64 * 64;
+        geo.sub = (uint32_t)((tile + S - 1) / S + 255) / 256 * 256;
         nblocks = geo.TW * S;
         lds = (size_t)Wd * hbins * 4;
     }
-    hipLaunchKernelGGL(k_msm_digits, dim3(nblocks), dim3(256), lds, st_, T, (uint32_t)total, p.c, Wd,
+    hipLaunchKernelGGL(k_msm_digits, dim3(nblocks), dim3(fused ? DIG_FUSED_THREADS : 256), lds, st_, T, (uint32_t)total, p.c, Wd,
                        (uint32_t)nmsm, (uint32_t)p.half, keys, vals, geo, (uint32_t)wstride);
     BPG_HIP(hipGetLastError());
     radix_sort(keys, vals, keys2, vals2, (int)p.key_bits, (const uint32_t *)tiles_.p, nt, (uint32_t *)sort_tmp_.p,
@@ -2724,6 +2728,20 @@ __global__ void k_gather_scalars(const sc *__restrict__ src, uint32_t count, uin
     sc a;
     sc_load(a, src + (size_t)j * stride + offset);
     sc_store(dst + j, a);
+}
+// dst[j] = src[idx[j]]
+__global__ void k_gather_idx(const sc *__restrict__ src, const uint32_t *__restrict__ idx, uint32_t count,
+                             sc *__restrict__ dst) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= count) return;
+    sc v;
+    sc_load(v, src + idx[j]);
+    sc_store(dst + j, v);
+}
+void launch_gather_idx(const ScD *src, const uint32_t *idx, uint32_t count, ScD *dst, hipStream_t st) {
+    if (!count) return;
+    hipLaunchKernelGGL(k_gather_idx, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(src), idx, count, AS_SC(dst));
+    BPG_HIP(hipGetLastError());
 }
 void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st) {
     if (!count) return;

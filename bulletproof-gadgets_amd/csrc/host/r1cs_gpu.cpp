@@ -779,34 +779,47 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
     if (P->prover) {
         // a_L, a_R, a_O: this rank's lanes i = j * world + rank
         const uint32_t nl = P->nl;
-        std::vector<ScD> tmp(nl ? nl : 1), tL;
+        static thread_local std::vector<ScD> tL, tmp;
+        static thread_local std::vector<uint32_t> iE, iD;
+        tL.resize(nl ? nl : 1);
+        tmp.resize(nl ? nl : 1);
         const uint8_t *src[3] = {cs->a_L, cs->a_R, cs->a_O};
         DBuf *dst[3] = {&P->aL, &P->aR, &P->aO};
         P->eq_split = false;
         for (int k = 0; k < 3; k++) {
+            std::vector<ScD> &t = k == 0 ? tL : tmp;
             for (uint32_t j = 0; j < nl; j++)
-                tmp[j] = to_dev(Scalar::reduce(src[k] + 32 * ((size_t)j * world + rank)));
-            up(*dst[k], tmp.data(), (size_t)nl * sizeof(ScD));
-            if (k == 0) tL = tmp;
+                t[j] = to_dev(Scalar::reduce(src[k] + 32 * ((size_t)j * world + rank)));
+            up(*dst[k], t.data(), (size_t)nl * sizeof(ScD));
             if (k == 1 && world == 1) {
-                // lanes with a_L == a_R: one A_I1 term on G_i + H_i
-                std::vector<ScD> sE, sL, sR;
-                std::vector<uint32_t> iE, iD;
-                for (uint32_t j = 0; j < nl; j++) {
-                    if (!memcmp(&tL[j], &tmp[j], sizeof(ScD))) { iE.push_back(j); sE.push_back(tL[j]); }
-                    else { iD.push_back(j); sL.push_back(tL[j]); sR.push_back(tmp[j]); }
-                }
+                // lanes with a_L == a_R: one A_I1 term on G_i + H_i. The host
+                // finds the lanes; the device gathers their scalars from the
+                // uploaded a_L / a_R
+                iE.clear(); iD.clear();
+                iE.reserve(nl); iD.reserve(nl);
+                for (uint32_t j = 0; j < nl; j++) (!memcmp(&tL[j], &t[j], sizeof(ScD)) ? iE : iD).push_back(j);
                 if (!iE.empty()) {
                     P->eq_split = true;
                     P->nE = (uint32_t)iE.size();
                     P->nD = (uint32_t)iD.size();
-                    up(P->eqS, sE.data(), sE.size() * sizeof(ScD));
                     up(P->eqI, iE.data(), iE.size() * 4);
-                    up(P->dfL, sL.data(), sL.size() * sizeof(ScD));
-                    up(P->dfR, sR.data(), sR.size() * sizeof(ScD));
                     up(P->dfI, iD.data(), iD.size() * 4);
+                    P->eqS.grow((size_t)P->nE * sizeof(ScD) + 4);
+                    P->dfL.grow((size_t)P->nD * sizeof(ScD) + 4);
+                    P->dfR.grow((size_t)P->nD * sizeof(ScD) + 4);
+                    hipStream_t st = producer_stage(device).st;
+                    launch_gather_idx(as<ScD>(P->aL), as<uint32_t>(P->eqI), P->nE, as<ScD>(P->eqS), st);
+                    launch_gather_idx(as<ScD>(P->aL), as<uint32_t>(P->dfI), P->nD, as<ScD>(P->dfL), st);
+                    launch_gather_idx(as<ScD>(P->aR), as<uint32_t>(P->dfI), P->nD, as<ScD>(P->dfR), st);
+                    BPG_HIP(hipStreamSynchronize(st));
                 }
             }
+        }
+        // the witness copies stay in this thread's buffers: wipe them (the
+        // barrier keeps the memset of a live buffer)
+        for (std::vector<ScD> *t : {&tL, &tmp}) {
+            memset(t->data(), 0, t->size() * sizeof(ScD));
+            __asm__ __volatile__("" : : "r"(t->data()) : "memory");
         }
         P->v.resize(m); P->vb.resize(m);
         std::vector<ScD> vbd(m ? m : 1);
