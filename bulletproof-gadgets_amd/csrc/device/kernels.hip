@@ -503,6 +503,25 @@ __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist,
 // keep, and equal keys are interchangeable in the MSM): keys are ranked
 // within their digit by LDS atomics instead of the wave ballots. Every later
 // pass must keep the order of the passes before it.
+// Exclusive scan of one value per thread over a 256-thread block, in thread
+// order: wave shuffles, then the four wave totals through `ws` (LDS, 4
+// words); two barriers (the second lets the caller reuse `ws`).
+DEVI uint32_t blk256_exscan(uint32_t v, uint32_t *ws) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0u;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    uint32_t before = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 3; q++) before += q < wave ? ws[q] : 0u;
+    __syncthreads();
+    return before + x - v;
+}
 template <int RS_BITS, bool STABLE>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                          int shift, const uint32_t *__restrict__ tiles, uint32_t nb,
@@ -511,9 +530,12 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
                                                          uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
     constexpr uint32_t RS_BINS = 1u << RS_BITS;
     WAVE_PRIO(BPG_SORT_PRIO);
-    __shared__ uint32_t base[RS_BINS], lstart[RS_BINS], tot[RS_BINS];
-    __shared__ uint32_t cnt[STABLE ? RS_ROUNDS : 1][RS_BLOCK / 64][RS_BINS];   // ballot ranking only
+    __shared__ uint32_t base[RS_BINS], lstart[RS_BINS], tot[RS_BINS], ws[4];
+    // ballot ranking only: per (round, wave) digit counts (<= 64), scanned in
+    // place into offsets within the iteration (< RS_ITER): 16 bits each
+    __shared__ uint16_t cnt[STABLE ? RS_ROUNDS : 1][RS_BLOCK / 64][RS_BINS];
     __shared__ uint32_t lk[RS_ITER], lv[RS_ITER];
+    static_assert(RS_BLOCK == 256 && RS_BINS <= 256 && RS_ITER < 65536, "blk256_exscan, 16-bit offsets");
     const uint32_t t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull);
     // Segmented by row: this tile's row occupies tiles [r0, r1) and elements
@@ -526,16 +548,9 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
     if (t < RS_BINS) {
         p0 = hist[t * nb + r0];
         cr = (r1 < nb ? hist[t * nb + r1] : total[t]) - p0;
-        lstart[t] = cr;
     }
-    __syncthreads();
-    for (uint32_t d = 1; d < RS_BINS; d <<= 1) {
-        uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
-        __syncthreads();
-        if (t < RS_BINS) lstart[t] += a;
-        __syncthreads();
-    }
-    if (t < RS_BINS) base[t] = rstart + lstart[t] - cr + (hist[t * nb + blockIdx.x] - p0);
+    const uint32_t rowpre = blk256_exscan(cr, ws);   // the row's digits before t
+    if (t < RS_BINS) base[t] = rstart + rowpre + (hist[t * nb + blockIdx.x] - p0);
     const uint64_t t0 = TL[0], t1 = TL[1];
     for (uint64_t it = t0; it < t1; it += RS_ITER) {
         uint32_t kk[RS_ROUNDS], vv[RS_ROUNDS], dd[RS_ROUNDS], rk[RS_ROUNDS];
@@ -553,15 +568,8 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
                 rk[r] = ok ? atomicAdd(&tot[d], 1u) : 0u;
             }
             __syncthreads();
-            if (t < RS_BINS) lstart[t] = tot[t];
-            __syncthreads();
-            for (uint32_t d = 1; d < RS_BINS; d <<= 1) {   // inclusive scan of tot -> exclusive starts
-                uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
-                __syncthreads();
-                if (t < RS_BINS) lstart[t] += a;
-                __syncthreads();
-            }
-            if (t < RS_BINS) lstart[t] -= tot[t];
+            const uint32_t ex = blk256_exscan(t < RS_BINS ? tot[t] : 0u, ws);   // exclusive starts
+            if (t < RS_BINS) lstart[t] = ex;
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < RS_ROUNDS; r++) {
@@ -573,8 +581,8 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
             }
             __syncthreads();
         } else {
-        uint32_t *cz = &cnt[0][0][0];
-        for (uint32_t j = t; j < RS_ROUNDS * (RS_BLOCK / 64) * RS_BINS; j += RS_BLOCK) cz[j] = 0;
+        uint32_t *cz = reinterpret_cast<uint32_t *>(&cnt[0][0][0]);
+        for (uint32_t j = t; j < RS_ROUNDS * (RS_BLOCK / 64) * RS_BINS / 2; j += RS_BLOCK) cz[j] = 0;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < RS_ROUNDS; r++) {
@@ -591,24 +599,17 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint32_t *__restr
                 m &= ((d >> b) & 1) ? bb : ~bb;
             }
             rk[r] = (uint32_t)__popcll(m & below);
-            if (ok && rk[r] == 0) cnt[r][wave][d] = (uint32_t)__popcll(m);
+            if (ok && rk[r] == 0) cnt[r][wave][d] = (uint16_t)__popcll(m);
         }
         __syncthreads();
+        uint32_t run = 0;
         if (t < RS_BINS) {   // offsets within the iteration, (round, wave) order
-            uint32_t run = 0;
             for (int r = 0; r < RS_ROUNDS; r++)
-                for (int w = 0; w < RS_BLOCK / 64; w++) { const uint32_t c = cnt[r][w][t]; cnt[r][w][t] = run; run += c; }
+                for (int w = 0; w < RS_BLOCK / 64; w++) { const uint32_t c = cnt[r][w][t]; cnt[r][w][t] = (uint16_t)run; run += c; }
             tot[t] = run;
-            lstart[t] = run;
         }
-        __syncthreads();
-        for (uint32_t d = 1; d < RS_BINS; d <<= 1) {   // inclusive scan of tot -> exclusive starts
-            uint32_t a = (t < RS_BINS && t >= d) ? lstart[t - d] : 0u;
-            __syncthreads();
-            if (t < RS_BINS) lstart[t] += a;
-            __syncthreads();
-        }
-        if (t < RS_BINS) lstart[t] -= tot[t];
+        const uint32_t ex = blk256_exscan(run, ws);   // exclusive starts (its barriers publish cnt, tot)
+        if (t < RS_BINS) lstart[t] = ex;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < RS_ROUNDS; r++) {
@@ -1049,10 +1050,10 @@ static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::gr
 #define DHIST_PARTS 16384
 #define DHIST_BYTES ((size_t)(RS_MAXTILES + (size_t)DHIST_PARTS * RS_MAXBINS) * 4)
 #define DIG_LDS_WORDS 8192   // fused histogram in LDS: windows x bins
-// fused launch: 1024-thread blocks (fewer parts per tile for the same
-// threads, so less hand-off traffic and a shorter last-part sum), ~512 blocks
-#define DIG_FUSED_THREADS 1024
-#define DIG_FUSED_BLOCKS 512
+// fused launch: ~2048 blocks of 256 threads (1024-thread blocks, fewer parts
+// per tile, measured 1.6% slower in the bench: profiles/r05k_ab.txt)
+#define DIG_FUSED_THREADS 256
+#define DIG_FUSED_BLOCKS 2048
 size_t MsmEngine::bytes() const {
     size_t b = 0;
     for (const DBuf *d : {&keys_, &vals_, &keys2_, &vals2_, &sort_tmp_, &tiles_, &rk_a_, &rk_b_, &rp_a_, &rp_b_,
@@ -1264,8 +1265,8 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     uint32_t *keys = (uint32_t *)keys_.p, *vals = (uint32_t *)vals_.p, *keys2 = (uint32_t *)keys2_.p, *vals2 = (uint32_t *)vals2_.p;
     ge *buckets = AS_GE(buckets_.p);
     // the first sort pass's histogram in the digit launch: one block per
-    // part of a tile of points (S parts, ~512 blocks of 1024 threads in
-    // all), each counting its W windows' keys in LDS
+    // part of a tile of points (S parts, ~2048 blocks in all), each counting
+    // its W windows' keys in LDS
     const uint32_t hbins = 1u << rs_bits((int)p.key_bits);
     const bool fused = geo.tiles && !fb && (uint64_t)Wd * hbins <= DIG_LDS_WORDS;
     uint32_t nblocks = nblk(total, 256);
