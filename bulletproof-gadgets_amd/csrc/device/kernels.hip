@@ -2220,16 +2220,14 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         if (op >> 15) gec_neg(c, c);
         ge_from_cached(acc, c);
     }
-    // table entries are loaded two ops ahead (the table lives past L2: one
-    // addition between load and use left the wave waiting on memory)
-    gec c, cn;
+    // the next op's table entry is loaded before the doublings
+    gec c;
     if (nops > 1) foldn_get(c, foldn_entry(tb, fold2_op(ops, 1)));
-    if (nops > 2) foldn_get(cn, foldn_entry(tb, fold2_op(ops, 2)));
     for (uint32_t k = 1; k < nops; k++) {
         const uint32_t op = fold2_op(ops, k);
         const uint32_t g = op & 255;
-        gec cnn;
-        if (k + 2 < nops) foldn_get(cnn, foldn_entry(tb, fold2_op(ops, k + 2)));
+        gec cn;
+        if (k + 1 < nops) foldn_get(cn, foldn_entry(tb, fold2_op(ops, k + 1)));
         if (g) {
             for (uint32_t j = 1; j < g; j++) ge_dbl_t<false>(acc, acc);
             ge_dbl_t<true>(acc, acc);
@@ -2239,7 +2237,6 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
         // profiles/r03j_ab_tskip_seglen.txt)
         if (op >> 15) ge_sub_c(acc, acc, c); else ge_add_c(acc, acc, c);
         c = cn;
-        cn = cnn;
     }
     const uint32_t tail = A.tail[sg];
     if (tail) {
