@@ -1283,7 +1283,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         geo.hpart = geo.htick + RS_MAXTILES;
         geo.hbins = hbins;
         geo.S = S;
-        geo.sub = (uint32_t)((tile + S - 1) / S + 255) / 256 * 256;
+        geo.sub = (uint32_t)((tile + S - 1) / S + 63) / 64 * 64;
         nblocks = geo.TW * S;
         lds = (size_t)Wd * hbins * 4;
     }

@@ -807,7 +807,10 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
                     P->eqS.grow((size_t)P->nE * sizeof(ScD) + 4);
                     P->dfL.grow((size_t)P->nD * sizeof(ScD) + 4);
                     P->dfR.grow((size_t)P->nD * sizeof(ScD) + 4);
-                    hipStream_t st = producer_stage(device).st;
+                    // the null stream, as the uploads above: a stream of its
+                    // own here would shift the process's stream -> hardware
+                    // queue assignment (measured -1.3%, profiles/r05m_ab.txt)
+                    hipStream_t st = nullptr;
                     launch_gather_idx(as<ScD>(P->aL), as<uint32_t>(P->eqI), P->nE, as<ScD>(P->eqS), st);
                     launch_gather_idx(as<ScD>(P->aL), as<uint32_t>(P->dfI), P->nD, as<ScD>(P->dfL), st);
                     launch_gather_idx(as<ScD>(P->aR), as<uint32_t>(P->dfI), P->nD, as<ScD>(P->dfR), st);
