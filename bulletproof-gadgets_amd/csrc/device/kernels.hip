@@ -1507,48 +1507,39 @@ void launch_lr_build(const ScD *aL, const ScD *aR, const ScD *sR, const ScD *wL,
     BPG_HIP(hipGetLastError());
 }
 
-// Block reductions of K scalars per thread: butterflies of lane shuffles
-// inside each wave (exact modular additions, so the order does not change
-// the sums), then the waves' sums through LDS -- two barriers for all K
-// columns instead of nine per column for an LDS tree.
-DEVI void sc_shfl_xor(sc &r, const sc &a, int m) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], m, 64);
-}
-// on return thread 0's v[k] hold the block's sums (blocks of <= 1024 threads)
-template <int K>
-DEVI void block_reduce_lds(sc (&v)[K]) {
-    __shared__ sc sh[K][16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
-    // unrolled: v[] stays in registers (a runtime index put it in scratch)
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            sc o;
-            sc_shfl_xor(o, v[k], m);
-            sc_add(v[k], v[k], o);
-        }
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < K; k++) sc_store(&sh[k][wave], v[k]);
-    }
-    __syncthreads();
-    if (tid == 0) {
-#pragma unroll
-        for (int k = 0; k < K; k++)
-            for (uint32_t w = 1; w < nw; w++) { sc a; sc_load(a, &sh[k][w]); sc_add(v[k], v[k], a); }
-    }
-    __syncthreads();   // sh may be rewritten by the caller's next reduction
-}
 // block reduction of K scalars per thread into partial[block*K + k]
 template <int K>
 DEVI void block_reduce_store(sc (&v)[K], sc *__restrict__ partial) {
-    block_reduce_lds<K>(v);
-    if (threadIdx.x == 0) {
+    __shared__ sc sh[256];
+    uint32_t tid = threadIdx.x;
+    // unrolled: v[] stays in registers (a runtime index put it in scratch)
 #pragma unroll
-        for (int k = 0; k < K; k++) sc_store(partial + blockIdx.x * K + k, v[k]);
+    for (int k = 0; k < K; k++) {
+        sc_store(&sh[tid], v[k]);
+        for (int s = 128; s >= 1; s >>= 1) {
+            __syncthreads();
+            if (tid < (uint32_t)s) { sc a, b; sc_load(a, &sh[tid]); sc_load(b, &sh[tid + s]); sc_add(a, a, b); sc_store(&sh[tid], a); }
+        }
+        __syncthreads();
+        if (tid == 0) { sc r; sc_load(r, &sh[0]); sc_store(partial + blockIdx.x * K + k, r); }
+        __syncthreads();
+    }
+}
+// LDS tree over the block: on return thread 0's v[k] hold the block's sums
+template <int K>
+DEVI void block_reduce_lds(sc (&v)[K]) {
+    __shared__ sc sh[256];
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        sc_store(&sh[tid], v[k]);
+        for (int s = 128; s >= 1; s >>= 1) {
+            __syncthreads();
+            if (tid < (uint32_t)s) { sc a, b; sc_load(a, &sh[tid]); sc_load(b, &sh[tid + s]); sc_add(a, a, b); sc_store(&sh[tid], a); }
+        }
+        __syncthreads();
+        if (tid == 0) sc_load(v[k], &sh[0]);
+        __syncthreads();
     }
 }
 #define RED_BLOCKS 1024
@@ -1579,6 +1570,7 @@ DEVI void block_reduce_final(sc (&v)[K], sc *__restrict__ partial, sc *__restric
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    __shared__ sc sh[256];
     __shared__ uint32_t last;
     const uint32_t tid = threadIdx.x, nb = gridDim.x;
     uint32_t *ticket = reinterpret_cast<uint32_t *>(partial + RED_TICKET);
@@ -1593,18 +1585,19 @@ DEVI void block_reduce_final(sc (&v)[K], sc *__restrict__ partial, sc *__restric
     }
     __syncthreads();
     if (!last) return;
-    sc acc[K];
 #pragma unroll
-    for (int k = 0; k < K; k++) sc_zero(acc[k]);
-    for (uint32_t b = tid; b < nb; b += blockDim.x) {
-#pragma unroll
-        for (int k = 0; k < K; k++) { sc t; sc_load(t, partial + (size_t)b * K + k); sc_add(acc[k], acc[k], t); }
-    }
-    block_reduce_lds<K>(acc);
-    if (tid == 0) {
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            sc r = acc[k];
+    for (int k = 0; k < K; k++) {
+        sc acc;
+        sc_zero(acc);
+        for (uint32_t b = tid; b < nb; b += blockDim.x) { sc t; sc_load(t, partial + (size_t)b * K + k); sc_add(acc, acc, t); }
+        sc_store(&sh[tid], acc);
+        for (int s = 128; s >= 1; s >>= 1) {
+            __syncthreads();
+            if (tid < (uint32_t)s) { sc x, y; sc_load(x, &sh[tid]); sc_load(y, &sh[tid + s]); sc_add(x, x, y); sc_store(&sh[tid], x); }
+        }
+        if (tid == 0) {
+            sc r;
+            sc_load(r, &sh[0]);
             if (mode == 0) {   // Montgomery-scaled partials: multiply back by R
                 sc r2;
                 for (int i = 0; i < 8; i++) r2.v[i] = SC_R2[i];
@@ -1614,8 +1607,9 @@ DEVI void block_reduce_final(sc (&v)[K], sc *__restrict__ partial, sc *__restric
             }
             sc_store(out + k, r);
         }
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+        __syncthreads();
     }
+    if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
 }
 // Montgomery-scaled sums (sum a*b/R); the final reduce multiplies by R^2/R
 __global__ __launch_bounds__(256) void k_tpoly(const sc *__restrict__ l1, const sc *__restrict__ l2,
