@@ -117,6 +117,10 @@ struct DBuf {
     void *p = nullptr;
     size_t cap = 0;
     void grow(size_t need);
+    // exactly `need` bytes on the first allocation (buffers whose size repeats,
+    // e.g. a recycled prepared statement's: no 25% slack counted against the
+    // HBM admission), as grow() after that
+    void grow_first_exact(size_t need);
 };
 // Partial-sum buffer of the reducing kernels (dot products, t(x), c_L / c_R,
 // huge flatten columns): 8192 scalars, the launch's reduction ticket at
@@ -306,8 +310,9 @@ void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv,
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st);
 // sharded prover: dst[j] = src[j * stride + offset]
 void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st);
-// dst[j] = src[idx[j]], j < count
-void launch_gather_idx(const ScD *src, const uint32_t *idx, uint32_t count, ScD *dst, hipStream_t st);
+// A_I1's split scalars: out = aL[eqI[0..nE)] | aL[dfI[0..nD)] | aR[dfI[0..nD)]
+void launch_eq_gather(const ScD *aL, const ScD *aR, const uint32_t *eqI, uint32_t nE, const uint32_t *dfI, uint32_t nD,
+                      ScD *out, hipStream_t st);
 void launch_gather_niels(const NielsD *src, uint32_t count, uint32_t stride, uint32_t offset, NielsD *dst,
                          hipStream_t st);
 // Montgomery -> canonical

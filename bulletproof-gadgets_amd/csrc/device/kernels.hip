@@ -1044,6 +1044,11 @@ void DBuf::grow(size_t need) {
     cap = n;
 }
 
+void DBuf::grow_first_exact(size_t need) {
+    if (p) { grow(need); return; }
+    BPG_HIP(hipMalloc(&p, need));
+    cap = need;
+}
 static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::grow's allocation
 // the digit launch's histogram hand-off: RS_MAXTILES tickets, then at most
 // DHIST_PARTS parts' counts of 256 bins
@@ -2730,18 +2735,23 @@ __global__ void k_gather_scalars(const sc *__restrict__ src, uint32_t count, uin
     sc_load(a, src + (size_t)j * stride + offset);
     sc_store(dst + j, a);
 }
-// dst[j] = src[idx[j]]
-__global__ void k_gather_idx(const sc *__restrict__ src, const uint32_t *__restrict__ idx, uint32_t count,
-                             sc *__restrict__ dst) {
+// A_I1's split scalars: out = aL[eqI[0..nE)] | aL[dfI[0..nD)] | aR[dfI[0..nD)]
+__global__ void k_eq_gather(const sc *__restrict__ aL, const sc *__restrict__ aR, const uint32_t *__restrict__ eqI,
+                            uint32_t nE, const uint32_t *__restrict__ dfI, uint32_t nD, sc *__restrict__ out) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= count) return;
+    if (j >= nE + 2 * nD) return;
+    const sc *src = j < nE + nD ? aL : aR;
+    const uint32_t i = j < nE ? eqI[j] : dfI[j < nE + nD ? j - nE : j - nE - nD];
     sc v;
-    sc_load(v, src + idx[j]);
-    sc_store(dst + j, v);
+    sc_load(v, src + i);
+    sc_store(out + j, v);
 }
-void launch_gather_idx(const ScD *src, const uint32_t *idx, uint32_t count, ScD *dst, hipStream_t st) {
+void launch_eq_gather(const ScD *aL, const ScD *aR, const uint32_t *eqI, uint32_t nE, const uint32_t *dfI, uint32_t nD,
+                      ScD *out, hipStream_t st) {
+    const uint32_t count = nE + 2 * nD;
     if (!count) return;
-    hipLaunchKernelGGL(k_gather_idx, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(src), idx, count, AS_SC(dst));
+    hipLaunchKernelGGL(k_eq_gather, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(aL), AS_CSC(aR), eqI, nE, dfI, nD,
+                       AS_SC(out));
     BPG_HIP(hipGetLastError());
 }
 void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st) {

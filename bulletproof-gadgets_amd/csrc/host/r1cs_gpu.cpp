@@ -405,7 +405,7 @@ void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_st
 static const size_t ROWS_HALF = 1024;   // pinned MSM row buffer: commitments [0, 1024), IPP L/R [1024, 2048)
 struct ProofBufs {
     DBuf wide, sL, sR, w, wloc, l1, r0, r1, r3, ypm, yipm, zlo, zhi, ylo, yhi, tabs, a, b, mscal, partial, Gp[2], Hp[2],
-        small, wG, wH, wconv, f3tab;
+        small, wG, wH, wconv, f3tab, eqsc;
     ScD *small_host = nullptr;   // pinned, 4096 scalars
     ScD *small_view = nullptr;   // its device view (kernels write c_L, c_R there)
     dev::ArgStage fold_stage, comb_stage, fold2_stage, fold3_stage;
@@ -635,7 +635,7 @@ static size_t workspace_bytes(const Workspace &ws) {
     for (const ProofBufs &B : ws.pb)
         for (const DBuf *d : {&B.wide, &B.sL, &B.sR, &B.w, &B.wloc, &B.l1, &B.r0, &B.r1, &B.r3, &B.ypm, &B.yipm,
                               &B.zlo, &B.zhi, &B.ylo, &B.yhi, &B.tabs, &B.a, &B.b, &B.mscal, &B.partial, &B.Gp[0],
-                              &B.Gp[1], &B.Hp[0], &B.Hp[1], &B.small, &B.wG, &B.wH, &B.wconv, &B.f3tab})
+                              &B.Gp[1], &B.Hp[0], &B.Hp[1], &B.small, &B.wG, &B.wH, &B.wconv, &B.f3tab, &B.eqsc})
             b += d->cap;
     return b;
 }
@@ -649,7 +649,7 @@ size_t consumer_bytes_estimate(const PreparedCS &cs, int P) {
     const size_t per_proof = 6 * grown(nl * S + 64) + grown(cs.ncol * S + 64) + 4 * grown(Nl * S + 64) +
                              grown((2 * Nl + 2) * S + 64) + 4 * grown(Nl / 2 * sizeof(PtD)) +
                              grown(ipp_fold3_table_bytes((uint32_t)std::max<size_t>(Nl / 32, 64), COMB_MAXRANGE)) +
-                             ((size_t)8 << 20);
+                             grown(2 * nl * S + 64) + ((size_t)8 << 20);
     const size_t msm = std::max(MsmEngine::job_bytes(2 * (uint64_t)Nl * P, 2 * P, MSM_NIELS),
                                 MsmEngine::job_bytes(5 * (uint64_t)nl, 3, MSM_NIELS));
     return (size_t)P * per_proof + msm;
@@ -694,8 +694,7 @@ PreparedCS::~PreparedCS() {
         memset(b, 0, host_slot_bytes);
         (void)hipHostFree(b);
     }
-    DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols,
-                    &eqS, &eqI, &dfL, &dfR, &dfI};
+    DBuf *bufs[] = {&aL, &aR, &aO, &vb_dev, &col_ptr, &col_row, &col_coeff, &short_cols, &long_cols, &eqI, &dfI};
     for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
 }
 
@@ -768,7 +767,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
     P->col_ptr_host = cnt;
     P->nshort = (uint32_t)sc_.size(); P->nlong = (uint32_t)lc_.size();
     auto up = [&](DBuf &d, const void *src, size_t bytes) {
-        d.grow(bytes ? bytes : 4);
+        d.grow_first_exact(bytes ? bytes : 4);
         if (bytes) BPG_HIP(hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice));
     };
     up(P->col_ptr, cnt.data(), cnt.size() * 4);
@@ -792,29 +791,19 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
                 t[j] = to_dev(Scalar::reduce(src[k] + 32 * ((size_t)j * world + rank)));
             up(*dst[k], t.data(), (size_t)nl * sizeof(ScD));
             if (k == 1 && world == 1) {
-                // lanes with a_L == a_R: one A_I1 term on G_i + H_i. The host
-                // finds the lanes; the device gathers their scalars from the
-                // uploaded a_L / a_R
+                // lanes with a_L == a_R: one A_I1 term on G_i + H_i
                 iE.clear(); iD.clear();
                 iE.reserve(nl); iD.reserve(nl);
                 for (uint32_t j = 0; j < nl; j++) (!memcmp(&tL[j], &t[j], sizeof(ScD)) ? iE : iD).push_back(j);
                 if (!iE.empty()) {
+                    // the lanes' scalars are gathered at commit time into
+                    // the proving thread's workspace (commit_a_segments):
+                    // a statement in flight holds only the lane indices
                     P->eq_split = true;
                     P->nE = (uint32_t)iE.size();
                     P->nD = (uint32_t)iD.size();
                     up(P->eqI, iE.data(), iE.size() * 4);
                     up(P->dfI, iD.data(), iD.size() * 4);
-                    P->eqS.grow((size_t)P->nE * sizeof(ScD) + 4);
-                    P->dfL.grow((size_t)P->nD * sizeof(ScD) + 4);
-                    P->dfR.grow((size_t)P->nD * sizeof(ScD) + 4);
-                    // the null stream, as the uploads above: a stream of its
-                    // own here would shift the process's stream -> hardware
-                    // queue assignment (measured -1.3%, profiles/r05m_ab.txt)
-                    hipStream_t st = nullptr;
-                    launch_gather_idx(as<ScD>(P->aL), as<uint32_t>(P->eqI), P->nE, as<ScD>(P->eqS), st);
-                    launch_gather_idx(as<ScD>(P->aL), as<uint32_t>(P->dfI), P->nD, as<ScD>(P->dfL), st);
-                    launch_gather_idx(as<ScD>(P->aR), as<uint32_t>(P->dfI), P->nD, as<ScD>(P->dfR), st);
-                    BPG_HIP(hipStreamSynchronize(st));
                 }
             }
         }
@@ -849,7 +838,7 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
 size_t prepared_bytes(const PreparedCS &cs) {
     size_t b = 0;
     for (const DBuf *d : {&cs.aL, &cs.aR, &cs.aO, &cs.vb_dev, &cs.col_ptr, &cs.col_row, &cs.col_coeff, &cs.short_cols,
-                          &cs.long_cols, &cs.eqS, &cs.eqI, &cs.dfL, &cs.dfR, &cs.dfI})
+                          &cs.long_cols, &cs.eqI, &cs.dfI})
         b += d->cap;
     std::lock_guard<std::mutex> lk(cs.slot_mu);
     return b + cs.slot_bufs.size() * cs.slot_bytes;
@@ -1208,7 +1197,7 @@ void rng_draw_multi(const PreparedCS *const *cs, const uint8_t *label, size_t la
 // draws is on the device (streamed up in chunks as it is drawn) and only
 // <s_R, H> is left when the last draw is made.
 static void commit_a_segments(const PreparedCS &cp, const GenSet &gs, bool split_ok, const void *G0, const void *H0,
-                              int64_t gneg, uint64_t gws, hipStream_t st, MsmSeg *sg, int &ns);
+                              int64_t gneg, uint64_t gws, hipStream_t st, DBuf &eqsc, MsmSeg *sg, int &ns);
 std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_t label_len,
                                const uint8_t entropy[32], ProveTimings *tm, const AllGather *ag) {
     if (!cs.prover) throw std::runtime_error("prepared circuit has no witness");
@@ -1231,7 +1220,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     if (nl) {
         MsmSeg sa[4];
         int ns = 0;
-        commit_a_segments(cs, *gs, !fbt, G0, H0, gneg, gws, ws.st, sa, ns);
+        commit_a_segments(cs, *gs, !fbt, G0, H0, gneg, gws, ws.st, B.eqsc, sa, ns);
         sa[ns++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws};
         int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
         pre.A = ws.msm->enqueue(sa, ns, 2, rows + CommitPre::ROWS_A, MSM_NIELS, rows_dev + CommitPre::ROWS_A);
@@ -1321,15 +1310,21 @@ static std::vector<Scalar> allgather_scalar_sums(const AllGather &ag, const Scal
 // H_i) and the others as two (a quarter fewer entries when half the lanes
 // are equal, as in a MiMC circuit), else the plain two segments.
 static void commit_a_segments(const PreparedCS &cp, const GenSet &gs, bool split_ok, const void *G0, const void *H0,
-                              int64_t gneg, uint64_t gws, hipStream_t st, MsmSeg *sg, int &ns) {
+                              int64_t gneg, uint64_t gws, hipStream_t st, DBuf &eqsc, MsmSeg *sg, int &ns) {
     const uint32_t nl = cp.nl;
     if (cp.eq_split && split_ok && cp.world == 1) {
         const dev::NielsD *GH = gh_table(gs, st);
-        if (cp.nE) sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.eqS)), GH, cp.nE, 0, gneg, 0,
-                               as<uint32_t>(const_cast<DBuf &>(cp.eqI))};
+        // the split's scalars, gathered from a_L / a_R by the prepared lane
+        // indices: a_L of the equal lanes, then a_L and a_R of the others
+        eqsc.grow(((size_t)cp.nE + 2 * (size_t)cp.nD) * sizeof(ScD) + 64);
+        ScD *eS = as<ScD>(eqsc), *dL = eS + cp.nE, *dR = dL + cp.nD;
+        launch_eq_gather(as<ScD>(const_cast<DBuf &>(cp.aL)), as<ScD>(const_cast<DBuf &>(cp.aR)),
+                         as<uint32_t>(const_cast<DBuf &>(cp.eqI)), cp.nE, as<uint32_t>(const_cast<DBuf &>(cp.dfI)),
+                         cp.nD, eS, st);
+        if (cp.nE) sg[ns++] = {eS, GH, cp.nE, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.eqI))};
         if (cp.nD) {
-            sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.dfL)), G0, cp.nD, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.dfI))};
-            sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.dfR)), H0, cp.nD, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.dfI))};
+            sg[ns++] = {dL, G0, cp.nD, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.dfI))};
+            sg[ns++] = {dR, H0, cp.nD, 0, gneg, 0, as<uint32_t>(const_cast<DBuf &>(cp.dfI))};
         }
         return;
     }
@@ -1446,7 +1441,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             const PreparedCS &cp = *csv[p];
             MsmSeg *sg = seg[p];
             int &ns = nseg[p];
-            commit_a_segments(cp, *gs, !fbt, G0, H0, gneg, gws, st, sg, ns);
+            commit_a_segments(cp, *gs, !fbt, G0, H0, gneg, gws, st, B.eqsc, sg, ns);
             sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.aO)), G0, nl, 1, gneg, gws};
             sg[ns++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
             sg[ns++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};

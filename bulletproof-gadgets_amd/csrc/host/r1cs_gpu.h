@@ -135,7 +135,7 @@ struct PreparedCS {
     // elsewhere (one rank only): compacted scalars and their lane indices
     bool eq_split = false;
     uint32_t nE = 0, nD = 0;
-    DBuf eqS, eqI, dfL, dfR, dfI;
+    DBuf eqI, dfI;   // lane indices of the A_I1 split (a_L == a_R, the others)
     DBuf col_ptr, col_row, col_coeff, short_cols, long_cols;
     uint32_t nshort = 0, nlong = 0, ncol = 0;
     std::vector<uint32_t> huge_cols, col_ptr_host;
