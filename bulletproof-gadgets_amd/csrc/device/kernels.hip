@@ -450,48 +450,48 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint32_t *__restrict
     if (threadIdx.x < RS_BINS) hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 // per digit d (one block each): exclusive scan of hist[d][0..nb) in place,
-// total[d] = the digit's count. 2048 counts per step: 8 consecutive per
-// thread summed serially, the threads' sums scanned by wave shuffles, the
-// four waves' totals through LDS (two barriers per step).
+// total[d] = the digit's count. 2048 counts per step, loaded up front
+// (coalesced, 8 per thread), then scanned 256 at a time: wave shuffles inside
+// each wave, the four waves' totals through LDS (double-buffered: one barrier
+// per 256 counts).
 #define RS_SCAN_K 8
 __global__ __launch_bounds__(256) void k_rs_colscan(uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ total) {
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[2][4];
     WAVE_PRIO(BPG_SORT_PRIO);
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint32_t *h = hist + (size_t)blockIdx.x * nb;
-    uint32_t carry = 0;
+    uint32_t carry = 0, par = 0;
     for (uint32_t r0 = 0; r0 < nb; r0 += 256 * RS_SCAN_K) {
-        const uint32_t i0 = r0 + t * RS_SCAN_K;
-        uint32_t v[RS_SCAN_K], sum = 0;
+        uint32_t v[RS_SCAN_K];
 #pragma unroll
         for (int k = 0; k < RS_SCAN_K; k++) {
-            v[k] = i0 + k < nb ? h[i0 + k] : 0u;
-            sum += v[k];
+            const uint32_t i = r0 + k * 256 + t;
+            v[k] = i < nb ? h[i] : 0u;
         }
-        uint32_t x = sum;   // inclusive scan over the wave
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            x += lane >= (uint32_t)d ? y : 0u;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t ws = wsum[q];
-            before += q < wave ? ws : 0u;
-            all += ws;
-        }
-        uint32_t run = carry + before + x - sum;
 #pragma unroll
         for (int k = 0; k < RS_SCAN_K; k++) {
-            if (i0 + k < nb) h[i0 + k] = run;
-            run += v[k];
+            if (r0 + k * 256 >= nb) break;   // uniform
+            uint32_t x = v[k];   // inclusive scan over the wave
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                x += lane >= (uint32_t)d ? y : 0u;
+            }
+            if (lane == 63) wsum[par][wave] = x;
+            __syncthreads();
+            uint32_t before = 0, all = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t ws = wsum[par][q];
+                before += q < wave ? ws : 0u;
+                all += ws;
+            }
+            const uint32_t i = r0 + k * 256 + t;
+            if (i < nb) h[i] = carry + before + x - v[k];
+            carry += all;
+            par ^= 1u;
         }
-        carry += all;
-        __syncthreads();   // wsum is rewritten by the next step
     }
     if (t == 0) total[blockIdx.x] = carry;
 }
