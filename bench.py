@@ -72,13 +72,18 @@ def parse():
     ap.add_argument("--msm-tables", type=int, default=-1, choices=(-1, 0, 1),
                     help="fixed-base generator tables for the MSMs over the generators (13 windows of 20 bits, "
                          "~7 GB at 2^20): 1 on, 0 or -1 (the default) off")
-    ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements"), default="prove",
+    ap.add_argument("--isolated-proofs", type=int, default=64,
+                    help="proofs of the isolated leg after the timed region (one consumer stream: the kernels' own "
+                         "chip time, the roofline's basis); 0 skips it")
+    ap.add_argument("--mode", choices=("prove", "verify", "verify-sharded", "latency", "statements", "isolated"),
+                    default="prove",
                     help="verify: Verifier::verify throughput over a batch of proofs made before timing "
                          "(config 5's batch verification); latency: one proof at a time, sharded over all "
                          "ranks (bpg_prove_prepared); verify-sharded: one verification at a time, its mega-MSM "
                          "split over all ranks; statements: distinct statements end to end through c_prove "
-                         "(parse + synthesis + upload + prove, prove.rs:37-82). Secondary lines, not the headline "
-                         "metric")
+                         "(parse + synthesis + upload + prove, prove.rs:37-82); isolated: only the isolated leg "
+                         "(one consumer stream), for a rocprofv3 trace of the kernels' own chip time. Secondary "
+                         "lines, not the headline metric")
     ap.add_argument("--cpu-leaves", type=int, default=16, help="leaves of the config-5-family CPU sample")
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="processes of the all-core CPU leg (default: the CPUs this job may use: the cgroup CPU "
@@ -115,12 +120,14 @@ def pmc_row(kernel):
     return row
 
 
-def prof_row(kernel):
+def prof_row(kernel, kind="profdefault"):
     """The average duration (us) and launch count of `kernel` in the latest
     committed rocprofv3 --kernel-trace --stats table of the bench's default
-    command (profiles/*_profdefault_kernels.md, scripts/prof_summary.py), or {}."""
+    command (profiles/*_profdefault_kernels.md) or of `bench.py --mode
+    isolated` (kind "isolated": profiles/*_isolated_kernels.md;
+    scripts/prof_summary.py), or {}."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_profdefault_kernels.md")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_%s_kernels.md" % kind)))
     if not files:
         return {}
     for line in open(files[-1]):
@@ -252,6 +259,83 @@ def heartbeat(period=20.0):
             time.sleep(period)
             print("bench: running, %.0f s" % (time.perf_counter() - t0), file=sys.stderr, flush=True)
     threading.Thread(target=run, daemon=True).start()
+
+
+class GpuTelemetry:
+    """GFX clock, socket power, hotspot temperature and GFX activity of this
+    rank's GPU sampled by amdsmi every `period` s between start() and stop()
+    (the timed region), so that a record carries the clock it ran at and
+    round-over-round numbers from different boxes can be told apart from a
+    box effect. Everything is optional: without amdsmi, or a metric the
+    device does not report, the line says so instead of failing."""
+
+    def __init__(self, torch, dev, period=0.25):
+        import threading
+        self.samples, self.err, self.h, self.period = [], None, None, period
+        self.stop_ev = threading.Event()
+        self.thread = None
+        try:
+            import amdsmi
+            self.smi = amdsmi
+            amdsmi.amdsmi_init(amdsmi.AmdSmiInitFlags.INIT_AMD_GPUS)
+            handles = amdsmi.amdsmi_get_processor_handles()
+            bus = getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None)
+            for h in handles:   # the handle on this rank's PCI bus ("dddd:bb:dd.f")
+                try:
+                    if bus is not None and int(amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")[1], 16) == bus:
+                        self.h = h
+                        break
+                except Exception:
+                    pass
+            if self.h is None and len(handles) == 1:
+                self.h = handles[0]
+            if self.h is None:
+                self.err = "no amdsmi handle on PCI bus %r (%d handles)" % (bus, len(handles))
+        except Exception as e:   # amdsmi absent or not permitted on this box
+            self.err = "amdsmi: %s" % e
+
+    @staticmethod
+    def _num(v):
+        return float(v) if isinstance(v, (int, float)) and not isinstance(v, bool) else None
+
+    def sample(self):
+        m = self.smi.amdsmi_get_gpu_metrics_info(self.h)
+        clks = [self._num(c) for c in (m.get("current_gfxclks") or []) if self._num(c)]
+        clk = (sum(clks) / len(clks)) if clks else (self._num(m.get("current_gfxclk")) or
+                                                    self._num(m.get("average_gfxclk_frequency")))
+        pw = self._num(m.get("current_socket_power")) or self._num(m.get("average_socket_power"))
+        return {"t": time.perf_counter(), "sclk_mhz": clk, "power_w": pw,
+                "temp_hotspot_c": self._num(m.get("temperature_hotspot")),
+                "gfx_activity_pct": self._num(m.get("average_gfx_activity"))}
+
+    def start(self):
+        import threading
+        if self.h is None:
+            return
+
+        def run():
+            while not self.stop_ev.is_set():
+                try:
+                    self.samples.append(self.sample())
+                except Exception as e:
+                    self.err = "amdsmi sample: %s" % e
+                    return
+                self.stop_ev.wait(self.period)
+        self.thread = threading.Thread(target=run, daemon=True)
+        self.thread.start()
+
+    def stop(self):
+        self.stop_ev.set()
+        if self.thread is not None:
+            self.thread.join(timeout=5)
+        out = {"samples": len(self.samples), "period_s": self.period, "source": "amdsmi gpu_metrics"}
+        if self.err:
+            out["error"] = self.err
+        for k in ("sclk_mhz", "power_w", "temp_hotspot_c", "gfx_activity_pct"):
+            vs = [s[k] for s in self.samples if s[k] is not None]
+            if vs:
+                out[k] = {"mean": round(sum(vs) / len(vs), 1), "min": round(min(vs), 1), "max": round(max(vs), 1)}
+        return out
 
 
 DIST_INFO = None
@@ -401,9 +485,11 @@ def main():
         return bench_verify(a, bpg, ctx, syn, prep, D, dist, rank, world, threads, entropies, q, n, N, W)
     if a.mode == "verify-sharded":
         return bench_verify_sharded(a, bpg, ctx, syn, prep, D, dist, rank, world, q, n, N, W)
+    L = bpg.lib()
+    if a.mode == "isolated":
+        return bench_isolated(a, prep, L, producers, rank, q, W)
     if a.warmup:
         prep.prove_batch(b"bench", sum((entropies(1000 + s) for s in range(a.warmup)), []), threads)
-    L = bpg.lib()
     L.bpg_profile_enable(0 if os.environ.get("BENCH_LIVE_TIMING") == "0" else 1)
     L.bpg_kernel_stats_reset()
 
@@ -412,7 +498,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    telem = GpuTelemetry(torch, dev)
     barrier()
+    telem.start()
     c0 = os.times()
     t0 = time.perf_counter()
     # the K steps' batches go through the producer/consumer pipeline as one
@@ -422,6 +510,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     c1 = os.times()
+    gpu_telemetry = telem.stop()
     pipe = bpg.last_batch_stats()
     host_busy = ((c1.user - c0.user) + (c1.system - c0.system)) / dt   # host cores kept busy by this rank
     if os.environ.get("BENCH_THREAD_CPU"):   # diagnostic: per-thread CPU seconds (utime, stime)
@@ -465,68 +554,13 @@ def main():
     if not ok:
         raise SystemExit("bench: a timed proof failed to verify")
 
-    # roofline of the dominant kernel (live HIP-event timing of single kernel
-    # launches inside the timed region, on the stream they run on)
-    def stat(name):
-        lc, ms, by, fm = ctypes.c_uint64(0), ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
-        L.bpg_kernel_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
-                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
-        L.bpg_kernel_femul.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
-        if L.bpg_kernel_stats(name.encode(), ctypes.byref(lc), ctypes.byref(ms), ctypes.byref(by)) != 0:
-            return None
-        L.bpg_kernel_femul(name.encode(), ctypes.byref(fm))
-        return lc.value, ms.value, by.value, fm.value
-    kernels = {k: stat(k) for k in KERNELS}
-    kernels = {k: v for k, v in kernels.items() if v}
-    jobs = {k: stat(k) for k in ("msm_commit", "msm_ipp")}
-    dom = max(kernels, key=lambda k: kernels[k][1]) if kernels else None
-    roof = None
-    if dom:
-        lc, ms, by, fm = kernels[dom]
-        sec = ms / lc / 1e3                      # average launch duration
-        achieved = (by / lc) / sec / 1e9         # GB/s of algorithmic bytes
-        pmc = pmc_row(KERNELS[dom])
-        prof = prof_row(KERNELS[dom])
-        # traffic: the PMC passes' HBM bytes per launch of the same kernel
-        # (FETCH_SIZE x 2 + WRITE_SIZE, separate passes); the PMC run's own
-        # algorithmic bytes per launch of that kernel (same label, same
-        # job mix) give the over-fetch ratio
-        pmc_alg = pmc.get("alg_bytes_per_launch")
-        roof = {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm",
-                # the HBM fraction is the metric's; the kernel is limited by its
-                # GF(p) multiply rate and gather latency, see "valu"
-                "limiter": "valu+gather-latency", "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": pmc.get("hbm_bytes_per_launch"), "launches": lc, "avg_launch_ms": round(sec * 1e3, 4),
-                "alg_bytes_per_launch": round(by / lc, 1),
-                "traffic_source": {"pmc_alg_bytes_per_launch": pmc_alg,
-                                   "traffic_over_alg": round(pmc["hbm_bytes_per_launch"] / pmc_alg, 2)
-                                   if pmc_alg and pmc.get("hbm_bytes_per_launch") else None,
-                                   "pmc_source": pmc.get("source")} if pmc else None,
-                # the kernels are VALU-bound (255-bit field arithmetic): the same
-                # launches against the measured GF(p) multiply peak
-                "valu": {"unit": "G fe_mul/s", "achieved": round(fm / lc / sec / 1e9, 2), "peak": FEMUL_PEAK_G,
-                         "frac": round(fm / lc / sec / 1e9 / FEMUL_PEAK_G, 4),
-                         "note": "per-launch time under the bench's concurrency (other streams share the CUs)"},
-                # the same kernel in isolation (PMC passes serialise dispatches):
-                # SQ_ACTIVE_INST_VALU share of the SIMDs' cycles, HBM GB/s
-                "pmc_isolated": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()
-                                 if k in ("avg_us", "valu_issue_share", "avg_waves_per_simd", "wave_wait_mem",
-                                          "hbm_gbs", "clock_ghz", "source")} or None,
-                # the same kernel's average launch in the committed rocprofv3
-                # kernel trace of this command (default host threads), and the
-                # HBM fraction that average gives
-                "rocprof_default_cmd": dict(prof, frac=round((by / lc) / (prof["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 6))
-                if prof else None,
-                "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
-                # every bracketed kernel: launches, average launch and
-                # algorithmic bytes per launch (scripts/pmc_table.py reads this
-                # table from its own run to pair the PMC bytes with them)
-                "kernel_table": {k: {"rocprof_name": KERNELS[k], "launches": v[0],
-                                     "avg_launch_ms": round(v[1] / v[0], 4),
-                                     "alg_bytes_per_launch": round(v[2] / v[0], 1)}
-                                 for k, v in kernels.items()},
-                "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items() if v}}
+    # roofline of the dominant kernel: live HIP-event timing of single kernel
+    # launches on the stream they run on, inside the timed region (under six
+    # streams' concurrency) and in the isolated leg below (one stream: the
+    # kernel's own chip time)
+    kernels, jobs = kernel_stats(L)
+    iso = isolated_leg(prep, L, producers, a.isolated_proofs, rank)
+    roof = roofline(kernels, jobs, iso, a.steps, dt / a.steps * 1e3)
 
     total_proofs = a.steps * batch * world
     value = total_proofs * q / dt
@@ -564,6 +598,9 @@ def main():
                                     "generators_from_disk_cache": setup["gens_from_cache"]},
         "device_phase_ms_single_proof": single_phases,
         "roofline": roof,
+        # this rank's GPU over the timed region (amdsmi): the clock and power
+        # a record ran at, so that box effects are visible
+        "gpu_telemetry": gpu_telemetry,
         "dist": DIST_INFO,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -572,6 +609,150 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def kernel_stats(L):
+    """Every bracketed kernel label's (launches, summed ms, algorithmic bytes,
+    fe_mul count) since the last bpg_kernel_stats_reset, and the two MSM job
+    labels'."""
+    L.bpg_kernel_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    L.bpg_kernel_femul.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
+
+    def stat(name):
+        lc, ms, by, fm = ctypes.c_uint64(0), ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
+        if L.bpg_kernel_stats(name.encode(), ctypes.byref(lc), ctypes.byref(ms), ctypes.byref(by)) != 0:
+            return None
+        L.bpg_kernel_femul(name.encode(), ctypes.byref(fm))
+        return (lc.value, ms.value, by.value, fm.value) if lc.value else None
+    kernels = {k: stat(k) for k in KERNELS}
+    jobs = {k: stat(k) for k in ("msm_commit", "msm_ipp")}
+    return {k: v for k, v in kernels.items() if v}, {k: v for k, v in jobs.items() if v}
+
+
+def isolated_leg(prep, L, producers, nproofs, rank):
+    """The kernels' own chip time: `nproofs` more proofs of the same batch
+    layout (four per lockstep step, so the same job mix per launch) through
+    ONE consumer thread, i.e. one HIP stream, so each bracketed launch has the
+    chip to itself (the producers only draw on the host and copy). Outside
+    the timed region; the timed region's brackets also count the time a
+    dispatch waits for CUs held by the other five streams' kernels."""
+    if nproofs <= 0:
+        return None
+    ents = [((rank << 40) | (1 << 39) | k).to_bytes(32, "little") for k in range(nproofs)]
+    # the library runs min(producers, groups of 8 proofs) producers: pool
+    # threads 0..P-1 draw, thread P proves. With 8 groups or more, P is the
+    # timed region's producer count and thread P its first consumer, whose
+    # four-proof workspace exists already (a thread that was a producer
+    # would allocate ~13 GB next to a full HBM)
+    P = max(1, min(producers, 8, (nproofs + 7) // 8))
+    L.bpg_kernel_stats_reset()
+    L.bpg_profile_enable(1)
+    t0 = time.perf_counter()
+    prep.prove_batch(b"bench", ents, P + 1)
+    wall = time.perf_counter() - t0
+    L.bpg_profile_enable(0)
+    import workloads as W
+    pipe = W._bpg().last_batch_stats()
+    if pipe["consumers"] != 1:
+        raise SystemExit("bench: the isolated leg ran %d consumer streams" % pipe["consumers"])
+    kernels, jobs = kernel_stats(L)
+    return {"kernels": kernels, "jobs": jobs, "proofs": nproofs, "wall_s": wall,
+            "consumers": pipe["consumers"], "lockstep": pipe["lockstep"]}
+
+
+def roofline(kernels, jobs, iso, steps, ms_per_step):
+    """The bench line's `roofline` object for the dominant kernel label (the
+    most bracketed device time in the timed region). `frac` is on the
+    kernel's own chip time (the isolated leg's average launch); the timed
+    region's concurrency-stretched average is `frac_concurrent`, and
+    `consistency` checks that launches per step x the average used fits in
+    a step."""
+    if not kernels:
+        return None
+    dom = max(kernels, key=lambda k: kernels[k][1])
+    lc, ms, by, fm = kernels[dom]
+    sec_c = ms / lc / 1e3                        # average launch under the bench's concurrency
+    alg = by / lc                                # algorithmic bytes per launch (SURVEY §8d units)
+    ik = (iso or {}).get("kernels", {}).get(dom)
+    if ik:
+        sec, alg_i, fm_i = ik[1] / ik[0] / 1e3, ik[2] / ik[0], ik[3] / ik[0]
+        basis = ("exclusive: the isolated leg's live HIP-event average (%d launches on one stream, %d proofs, "
+                 "%d proofs per step), the kernel alone on the chip" % (ik[0], iso["proofs"], iso["lockstep"]))
+    else:
+        sec, alg_i, fm_i = sec_c, alg, fm / lc
+        basis = "concurrent: no isolated leg (--isolated-proofs 0)"
+    achieved = alg_i / sec / 1e9
+    pmc = pmc_row(KERNELS[dom])
+    prof = prof_row(KERNELS[dom])
+    iprof = prof_row(KERNELS[dom], "isolated")
+    pmc_alg = pmc.get("alg_bytes_per_launch")
+    per_step = lc / max(steps, 1)
+    return {"kernel": dom, "rocprof_name": KERNELS[dom], "bound": "hbm",
+            # the HBM fraction is the metric's; the kernel is limited by its
+            # GF(p) multiply rate and gather latency (DESIGN.md (d)), see "valu"
+            "limiter": "valu+gather-latency", "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+            "basis": basis, "avg_launch_ms": round(sec * 1e3, 4), "alg_bytes_per_launch": round(alg_i, 1),
+            # the same kernel's launches in the timed region, each bracket
+            # stretched by the other streams' kernels holding CUs
+            "frac_concurrent": round(alg / sec_c / 1e9 / HBM_PEAK_GBS, 6),
+            "avg_launch_ms_concurrent": round(sec_c * 1e3, 4), "launches": lc,
+            "alg_bytes_per_launch_timed": round(alg, 1),
+            "consistency": {"launches_per_step": round(per_step, 1), "ms_per_step": round(ms_per_step, 2),
+                            "launches_x_avg_ms": round(per_step * sec * 1e3, 1),
+                            "launches_x_avg_concurrent_ms": round(per_step * sec_c * 1e3, 1),
+                            "ok": per_step * sec * 1e3 <= ms_per_step,
+                            "share_of_step": round(per_step * sec * 1e3 / ms_per_step, 4)},
+            "traffic": pmc.get("hbm_bytes_per_launch"),
+            "traffic_source": {"pmc_alg_bytes_per_launch": pmc_alg,
+                               "traffic_over_alg": round(pmc["hbm_bytes_per_launch"] / pmc_alg, 2)
+                               if pmc_alg and pmc.get("hbm_bytes_per_launch") else None,
+                               "pmc_avg_us": pmc.get("avg_us"),
+                               "pmc_source": pmc.get("source")} if pmc else None,
+            # the kernels are VALU-bound (255-bit field arithmetic): the same
+            # launches against the measured GF(p) multiply peak
+            "valu": {"unit": "G fe_mul/s", "achieved": round(fm_i / sec / 1e9, 2), "peak": FEMUL_PEAK_G,
+                     "frac": round(fm_i / sec / 1e9 / FEMUL_PEAK_G, 4),
+                     "frac_concurrent": round(fm / lc / sec_c / 1e9 / FEMUL_PEAK_G, 4)},
+            # the same kernel in the committed PMC passes (which serialise
+            # dispatches): SQ_ACTIVE_INST_VALU share of the SIMDs' cycles, HBM GB/s
+            "pmc_isolated": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pmc.items()
+                             if k in ("avg_us", "valu_issue_share", "avg_waves_per_simd", "wave_wait_mem",
+                                      "hbm_gbs", "clock_ghz", "source")} or None,
+            # the committed rocprofv3 kernel traces of `bench.py --mode
+            # isolated` (must agree with avg_launch_ms) and of the default
+            # command (must agree with avg_launch_ms_concurrent)
+            "rocprof_isolated_cmd": iprof or None,
+            "rocprof_default_cmd": prof or None,
+            "device_ms_by_kernel": {k: round(v[1], 2) for k, v in kernels.items()},
+            # every bracketed kernel: launches, average launch (timed region and
+            # isolated leg) and algorithmic bytes per launch
+            "kernel_table": {k: {"rocprof_name": KERNELS[k], "launches": v[0],
+                                 "avg_launch_ms": round(v[1] / v[0], 4),
+                                 "avg_launch_ms_isolated": round(iso["kernels"][k][1] / iso["kernels"][k][0], 4)
+                                 if iso and k in iso["kernels"] else None,
+                                 "alg_bytes_per_launch": round(v[2] / v[0], 1)}
+                             for k, v in kernels.items()},
+            "device_ms_by_msm_job": {k: round(v[1], 2) for k, v in jobs.items()},
+            "isolated_leg": {"proofs": iso["proofs"], "wall_s": round(iso["wall_s"], 2),
+                             "consumers": iso["consumers"], "proofs_per_step": iso["lockstep"]} if iso else None}
+
+
+def bench_isolated(a, prep, L, producers, rank, q, W):
+    """`--mode isolated`: only the isolated leg (warm-up included: one
+    consumer stream), for a rocprofv3 kernel trace whose per-kernel averages
+    are the line's exclusive launch times (profiles/*_isolated_kernels.md)."""
+    if a.warmup:   # the same layout once (comb tables, the consumer's workspace)
+        isolated_leg(prep, L, producers, a.isolated_proofs, rank)
+    iso = isolated_leg(prep, L, producers, a.isolated_proofs, rank)
+    out = {"metric": "isolated leg: kernel launches on one stream (no concurrency)", "proofs": iso["proofs"],
+           "wall_s": round(iso["wall_s"], 2), "constraints_per_s": round(iso["proofs"] * q / iso["wall_s"], 1),
+           "kernel_table": {k: {"rocprof_name": KERNELS[k], "launches": v[0], "avg_launch_ms": round(v[1] / v[0], 4),
+                                "alg_bytes_per_launch": round(v[2] / v[0], 1)} for k, v in iso["kernels"].items()},
+           "config": {"workload": W.NAMES[a.config]}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def pipeline_line(p, ncpu, per_rank, pinned, nproofs):
@@ -591,7 +772,8 @@ def pipeline_line(p, ncpu, per_rank, pinned, nproofs):
             "proofs_per_s": round(nproofs / (p["wall_ms"] / 1e3), 2),
             "consumers_by_threads": p["consumers_by_threads"], "consumers_by_hbm": p["consumers_by_hbm"],
             "hw_queues": p["hw_queues"],
-            "est_gb_per_consumer": round(p["est_gb_per_consumer"], 2), "hbm_free_gb_at_start": round(p["hbm_free_gb"], 1),
+            "est_gb_per_consumer": round(p["est_gb_per_consumer"], 2), "ws_gb_max": round(p.get("ws_gb_max", 0), 2),
+            "hbm_free_gb_at_start": round(p["hbm_free_gb"], 1),
             "cpus": {"job": ncpu, "rank_share": per_rank, "process": p["process_cpus"], "pinned": pinned or None}}
 
 

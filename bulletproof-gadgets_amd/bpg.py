@@ -581,7 +581,8 @@ def last_timings():
 
 BATCH_STATS = ("producers", "consumers", "lockstep", "inflight", "wall_ms", "fill_ms", "consumer_starved_ms",
                "producer_slot_wait_ms", "producer_draw_ms", "consumer_prove_ms", "host_bound", "hbm_free_gb",
-               "est_gb_per_consumer", "consumers_by_threads", "consumers_by_hbm", "process_cpus", "hw_queues")
+               "est_gb_per_consumer", "consumers_by_threads", "consumers_by_hbm", "process_cpus", "hw_queues",
+               "ws_gb_max")
 
 
 def last_batch_stats():
@@ -598,7 +599,7 @@ def last_batch_stats():
 
 STATEMENTS_STATS = ("workers", "consumers", "limit", "wall_ms", "synth_ms", "prepare_ms", "rng_ms", "prove_ms",
                     "worker_idle_ms", "consumer_idle_ms", "bound_stage", "hbm_limit", "est_gb_per_statement",
-                    "lockstep", "hbm_free_gb", "oom_retired")
+                    "lockstep", "hbm_free_gb", "oom_retired", "est_gb_per_device_thread", "ws_gb_max")
 
 
 def last_statements_stats():

@@ -2932,7 +2932,7 @@ void launch_cached_to_niels(const PtD *const *in, NielsD *const *out, int nvec, 
                        count);
     BPG_HIP(hipGetLastError());
 }
-__global__ void k_gen_sum(const gen *__restrict__ G, const gen *__restrict__ H, gec *__restrict__ out, uint32_t count) {
+__global__ __launch_bounds__(64) void k_gen_sum(const gen *__restrict__ G, const gen *__restrict__ H, gec *__restrict__ out, uint32_t count) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     gen g, h;

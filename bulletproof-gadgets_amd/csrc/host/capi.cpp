@@ -650,11 +650,12 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                 fail(e.what());
             }
         });
+        size_t ws_max = 0;   // the largest consumer workspace after the call (vs est_c)
         {
             std::lock_guard<std::mutex> lk(g_held_mu);
             std::vector<size_t> &h = g_held[cs.device];
             if (h.size() < P + C) h.resize(P + C, 0);
-            for (uint32_t id = P; id < P + C; id++) h[id] = held_after[id];
+            for (uint32_t id = P; id < P + C; id++) { h[id] = held_after[id]; ws_max = std::max(ws_max, held_after[id]); }
         }
         const double wall = since_ms(t_start);
         {
@@ -666,7 +667,7 @@ int bpg_prove_batch(bpg_prepared *p, const uint8_t *label, size_t label_len, con
                                                starve_ms, slot_wait_ms, draw_ms, prove_ms,
                                                starve_ms / span > 0.10 ? 1.0 : 0.0, free_b / 1e9, est_c / 1e9,
                                                (double)C_req, (double)C_hbm, (double)process_cpus(),
-                                               (double)hw_queues()};
+                                               (double)hw_queues(), ws_max / 1e9};
             memcpy(g_bs, v, sizeof(v));
         }
         if (!err.empty()) throw std::runtime_error(err);
@@ -700,7 +701,7 @@ static ProofArtifacts *make_artifacts(const std::string &coms, const std::vector
 namespace {
 std::atomic<uint32_t> g_stmt_consumers(0), g_stmt_lockstep(0);   // bpg_set_statements_layout (0: defaults)
 std::mutex g_ss_mu;
-double g_ss[16] = {0};   // bpg_last_statements_stats
+double g_ss[18] = {0};   // bpg_last_statements_stats
 }  // namespace
 int bpg_prove_statements(const char *name, const char *const *instances, const char *const *witnesses,
                          const char *const *gadgets, const uint64_t *seeds, uint32_t count, uint32_t threads,
@@ -758,7 +759,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
         // what HBM holds next to the consumers' workspaces, sized once the
         // first statement is prepared (until then at most W)
         uint32_t limit = 4 * W + 8 + 2 * C, hbm_limit = 0, C_eff = C;
-        double est_st = 0, adm_free_b = 0;
+        double est_st = 0, adm_free_b = 0, per_c_est = 0;
         double synth_ms = 0, prep_ms = 0, rng_ms = 0, prove_ms = 0, widle_ms = 0, cidle_ms = 0;
         std::string first_err;
         bool fatal = false;
@@ -894,6 +895,7 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
                             c_fit = 1;
                         }
                         C_eff = c_fit;
+                        per_c_est = per_c;
                         consumers_left = C_eff;
                         hbm_limit = (uint32_t)std::max<double>(std::min<double>(C_eff * L + 8, limit),
                                                                (all - C_eff * per_c) / est_st);
@@ -982,11 +984,12 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             }
             if (!worker) held_after[id] = thread_workspace_bytes(device);
         });
+        size_t ws_max = 0;   // the largest device-thread workspace after the call (vs the estimate)
         {
             std::lock_guard<std::mutex> lk(g_held_mu);
             std::vector<size_t> &h = g_held[device];
             if (h.size() < W + C) h.resize(W + C, 0);
-            for (uint32_t id = W; id < W + C; id++) h[id] = held_after[id];
+            for (uint32_t id = W; id < W + C; id++) { h[id] = held_after[id]; ws_max = std::max(ws_max, held_after[id]); }
         }
         spare.clear();   // the recycled statements' device memory, freed once per call
         {
@@ -997,9 +1000,9 @@ int bpg_prove_statements(const char *name, const char *const *instances, const c
             const double wbusy = 1.0 - widle_ms / std::max(1e-9, wall * W);
             const double cbusy = 1.0 - cidle_ms / std::max(1e-9, wall * C_eff);
             const int bound = wbusy >= cbusy ? 1 : 2;
-            const double v[16] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
+            const double v[18] = {(double)W, (double)C_eff, (double)limit, wall, synth_ms, prep_ms, rng_ms, prove_ms,
                                   widle_ms, cidle_ms, (double)bound, (double)hbm_limit, est_st / 1e9, (double)L,
-                                  adm_free_b / 1e9, (double)oom_retired};
+                                  adm_free_b / 1e9, (double)oom_retired, per_c_est / 1e9, ws_max / 1e9};
             std::lock_guard<std::mutex> lk(g_ss_mu);
             memcpy(g_ss, v, sizeof(v));
         }
@@ -1026,7 +1029,7 @@ int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep) {
 }
 int bpg_last_statements_stats(double *out, int n) {
     std::lock_guard<std::mutex> lk(g_ss_mu);
-    for (int i = 0; i < n && i < 16; i++) out[i] = g_ss[i];
+    for (int i = 0; i < n && i < 18; i++) out[i] = g_ss[i];
     return 0;
 }
 

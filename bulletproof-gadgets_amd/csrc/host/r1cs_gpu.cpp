@@ -122,12 +122,17 @@ const dev::NielsD *gh_table(const GenSet &gs, hipStream_t st) {
         (void)hipFree(gh);
         throw HipError(hipErrorOutOfMemory, "hipMalloc(G + H staging)", __FILE__, __LINE__);
     }
-    launch_gen_sum(gs.G, gs.H, tmp, gs.N, st);
+    // prepare_cs builds it with no stream of its own: a private one
+    hipStream_t own = nullptr;
+    if (!st) BPG_HIP(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    const hipStream_t s = st ? st : own;
+    launch_gen_sum(gs.G, gs.H, tmp, gs.N, s);
     const PtD *in[1] = {tmp};
     dev::NielsD *out[1] = {gh};
-    launch_cached_to_niels(in, out, 1, gs.N, st);
-    launch_niels_neg(gh, gh + gs.N, gs.N, st);
-    BPG_HIP(hipStreamSynchronize(st));
+    launch_cached_to_niels(in, out, 1, gs.N, s);
+    launch_niels_neg(gh, gh + gs.N, gs.N, s);
+    BPG_HIP(hipStreamSynchronize(s));
+    if (own) (void)hipStreamDestroy(own);
     (void)hipFree(tmp);
     gs.GH = gh;
     return gh;
@@ -417,7 +422,8 @@ struct ProofBufs {
         }
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&wide, &sL, &sR, &w, &wloc, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs,
-                        &a, &b, &mscal, &partial, &Gp[0], &Gp[1], &Hp[0], &Hp[1], &small, &wG, &wH, &wconv, &f3tab};
+                        &a, &b, &mscal, &partial, &Gp[0], &Gp[1], &Hp[0], &Hp[1], &small, &wG, &wH, &wconv, &f3tab,
+                        &eqsc};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
     }
 };
@@ -646,13 +652,29 @@ static size_t grown(size_t need) { return need + need / 4 + 256; }   // DBuf::gr
 // proof, the commitments 5 nl per proof in their own jobs).
 size_t consumer_bytes_estimate(const PreparedCS &cs, int P) {
     const size_t S = sizeof(ScD), nl = cs.nl, Nl = cs.Nl;
+    // the first triple fold's table: level 2 -> 5 (Nl / 32 output lanes)
+    // after the comb pass, but level 0 -> 3 (Nl / 8, four times the table:
+    // 1.2 GB per 2^20 proof) when this device holds no comb tables for the
+    // circuit (e.g. next to a foreign allocation). Round 5's estimate always
+    // assumed the former, so a statements call without tables admitted
+    // device threads that ran out of HBM in their first fold
+    bool comb = false;
+    if (cs.strat.tables()) {
+        DeviceContext &c = DeviceContext::get(cs.device);
+        std::lock_guard<std::mutex> lk(c.mu);
+        comb = c.combs.count(std::make_tuple(Nl, cs.rank, cs.world)) != 0;
+    }
+    const size_t hq = std::max<size_t>(comb ? Nl / 32 : Nl / 8, 64);
     const size_t per_proof = 6 * grown(nl * S + 64) + grown(cs.ncol * S + 64) + 4 * grown(Nl * S + 64) +
                              grown((2 * Nl + 2) * S + 64) + 4 * grown(Nl / 2 * sizeof(PtD)) +
-                             grown(ipp_fold3_table_bytes((uint32_t)std::max<size_t>(Nl / 32, 64), COMB_MAXRANGE)) +
+                             grown(ipp_fold3_table_bytes((uint32_t)hq, COMB_MAXRANGE)) +
                              grown(2 * nl * S + 64) + ((size_t)8 << 20);
+    // generator_range_sum's unit scalars (round 0's padding lanes, once per
+    // generator set; at most Nl / 2 of them) in the workspace
+    const size_t ones = grown(Nl / 2 * S + 64);
     const size_t msm = std::max(MsmEngine::job_bytes(2 * (uint64_t)Nl * P, 2 * P, MSM_NIELS),
                                 MsmEngine::job_bytes(5 * (uint64_t)nl, 3, MSM_NIELS));
-    return (size_t)P * per_proof + msm;
+    return (size_t)P * per_proof + ones + msm;
 }
 // Verifier::verify of a circuit of cs's size on a fresh workspace: the
 // mega-MSM over 2N generators and the flattened / y^-i / g-h vectors.
@@ -807,11 +829,18 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
                 }
             }
         }
-        // the witness copies stay in this thread's buffers: wipe them (the
-        // barrier keeps the memset of a live buffer)
+        // the witness copies: wiped (the barrier keeps the memset of a live
+        // buffer) and released, not kept per thread (64 MB per worker at
+        // 2^20); the equal-lane lists derive from the witness too
         for (std::vector<ScD> *t : {&tL, &tmp}) {
             memset(t->data(), 0, t->size() * sizeof(ScD));
             __asm__ __volatile__("" : : "r"(t->data()) : "memory");
+            std::vector<ScD>().swap(*t);
+        }
+        for (std::vector<uint32_t> *t : {&iE, &iD}) {
+            memset(t->data(), 0, t->size() * sizeof(uint32_t));
+            __asm__ __volatile__("" : : "r"(t->data()) : "memory");
+            std::vector<uint32_t>().swap(*t);
         }
         P->v.resize(m); P->vb.resize(m);
         std::vector<ScD> vbd(m ? m : 1);
@@ -829,6 +858,10 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
         // circuit-independent, outside any timed region
         DeviceContext &ctx = DeviceContext::get(device);
         std::shared_ptr<const GenSet> gs = ctx.gens(P->N, rank, world);
+        // the A_I1 split's G_i + H_i table (256 MB at 2^20, 160 MB of staging
+        // while it is built) now, before any caller's HBM admission reads the
+        // free memory: never allocated mid-proof
+        if (P->eq_split) gh_table(*gs, nullptr);
         if (strat.fixed_base()) ctx.fb(gs, P->N);
         if (strat.tables()) ctx.comb(gs, P->Nl);
     }
@@ -1244,16 +1277,33 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     rb.on_device = true;
     rb.stage = ws.s_host;
     RngBlock *rbp = &rb;
+    // s_host receives this proof's s_L / s_R draws. On success it is zeroed
+    // on the stream that read them, waited for by the next proof
+    // before it draws; when the draw or the device part throws, this guard
+    // waits for both streams and zeroes it on the host
+    struct WipeOnError {
+        Workspace &ws;
+        int device;
+        size_t bytes;
+        bool armed = true;
+        ~WipeOnError() {
+            if (!armed) return;
+            (void)hipStreamSynchronize(producer_stage(device).st);
+            (void)hipStreamSynchronize(ws.st);
+            (void)hipGetLastError();
+            memset(ws.s_host, 0, bytes);
+            __asm__ __volatile__("" : : "r"(ws.s_host) : "memory");
+        }
+    } wipe{ws, cs.device, 2 * (size_t)n * 64};
     rng_draw_group(cs, label, label_len, &entropy, 1, &rbp, true, &progress);
     double t1 = now_ms();
     ProveTimings t;
     const RngBlock *crb = &rb;
     std::vector<uint8_t> pr = gpu_prove_lockstep(cs, label, label_len, &crb, 1, &t, ag, &pre)[0];
-    // s_host holds this proof's s_L / s_R draws: zeroed on the stream that
-    // read them, waited for by the next proof before it draws
     if (!ws.stage_wiped) BPG_HIP(hipEventCreateWithFlags(&ws.stage_wiped, hipEventBlockingSync | hipEventDisableTiming));
     BPG_HIP(hipMemsetAsync(ws.s_host, 0, 2 * (size_t)n * 64, ws.st));
     BPG_HIP(hipEventRecord(ws.stage_wiped, ws.st));
+    wipe.armed = false;
     t.rng_ms = t1 - t0;
     t.total_ms += t1 - t0;
     last_timings() = t;
@@ -1335,6 +1385,22 @@ static void commit_a_segments(const PreparedCS &cp, const GenSet &gs, bool split
 // sum_{j in [a, b)} H_j of a generator set (one MSM with unit scalars on the
 // workspace's stream, once per range; rows land in the commitment half of the
 // pinned row buffer, which is free once the commitments are combined).
+// Test hook (tests/test_gpu_robustness.py): with BPG_TEST_INJECT_OOM=<k> the
+// first proof of the process to reach IPP round k throws hipErrorOutOfMemory
+// there, once, half way through gpu_prove_lockstep, as a workspace that
+// cannot grow would (the statements path's device-thread retirement).
+static uint32_t inject_oom_round() {
+    static const uint32_t r = [] {
+        const char *e = getenv("BPG_TEST_INJECT_OOM");
+        return e && *e ? (uint32_t)atoi(e) : ~0u;
+    }();
+    return r;
+}
+static void inject_oom_once() {
+    static std::atomic<bool> fired(false);
+    if (!fired.exchange(true)) throw HipError(hipErrorOutOfMemory, "injected (BPG_TEST_INJECT_OOM)", __FILE__, __LINE__);
+}
+
 static Point generator_range_sum(Workspace &ws, const GenSet &gs, uint32_t a, uint32_t b) {
     {
         std::lock_guard<std::mutex> lk(gs.sums_mu);
@@ -1667,6 +1733,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
     uint32_t k = 0;
     for (; len != 1; k++) {
         const uint32_t h = len / 2;
+        if (k == inject_oom_round()) inject_oom_once();
         if (!tail && depth == 0 && cur >= 0 && len <= tail_len && len >= (sharded ? 2u : 4u)) {
             tail = true;
             M = len;

@@ -105,9 +105,11 @@ int bpg_set_statements_layout(uint32_t consumers, uint32_t lockstep);
  * layout's lockstep, lowered when HBM does not hold one device thread of
  * that many), [14] free HBM (GB) when the admission was made, [15] device
  * threads that retired because their workspace could not grow (their
- * statements were proved by the others). A call whose free HBM does not hold
- * one device thread of one statement fails before proving with an error
- * saying so (out[k] all NULL). (n <= 16) */
+ * statements were proved by the others), [16] the admission's estimate of a
+ * device thread's workspace (GB), [17] the largest device-thread workspace
+ * after the call (GB). A call whose free HBM does not hold one device thread
+ * of one statement fails before proving with an error saying so (out[k] all
+ * NULL). (n <= 18) */
 int bpg_last_statements_stats(double *out, int n);
 
 /* Added: `prover.num_constraints()` of the last c_prove on this thread
@@ -382,8 +384,9 @@ int bpg_ctx_set_pipeline(bpg_ctx *ctx, uint32_t producers, uint32_t lockstep,
  * hardware queues HIP gives the process (GPU_MAX_HW_QUEUES when HIP
  * initialised, else HIP's default 4): consumers are at most that many, one
  * stream per queue. Export GPU_MAX_HW_QUEUES=16 before anything initialises
- * HIP for the full layout. */
-#define BPG_BATCH_STATS 17
+ * HIP for the full layout. [17] the largest consumer
+ * workspace after the call (GB; [12] is the admission's estimate of it). */
+#define BPG_BATCH_STATS 18
 int bpg_last_batch_stats(double *out, int n);
 
 /* Verifier::verify (src/verify.rs:71) over `count` proofs of one circuit

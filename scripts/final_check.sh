@@ -6,7 +6,8 @@
 #       same build (one counter group per pass, kernel trace only) over the
 #       default layout at 48 proofs per step, reduced to a per-kernel table
 #       that pairs each kernel's HBM bytes with its algorithmic bytes from the
-#       same run
+#       same run; and `bench.py --mode isolated` (one consumer stream) under
+#       the same trace: the kernels' own chip time, the roofline's basis
 #   R=<tag> bash scripts/final_check.sh modes   the driver's bench command, then
 #       the secondary modes (verify, verify-sharded, latency, statements) and
 #       the --gpus launcher with two self-spawned ranks sharing the one GPU
@@ -21,6 +22,12 @@ if [ "$1" = prof ]; then
   db=$(find /tmp/${R}_prof -name '*.db' -print -quit)
   python3 scripts/prof_summary.py "$db" gpurun_out/${R}_profdefault_kernels.md > /dev/null || exit $?
   python3 scripts/timeline.py "$db" 0.35 gpurun_out/${R}_timeline_default.md 0.92 > /dev/null || exit $?
+  # the isolated leg alone (one consumer stream): the per-kernel averages the
+  # bench line's roofline.frac uses (avg_launch_ms) must agree with this table
+  (cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/${R}_iso && \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/${R}_iso -o run -- python3 $ROOTD/bench.py --mode isolated --warmup 1 > $ROOTD/gpurun_out/${R}_isolated_bench.json 2> $ROOTD/gpurun_out/${R}_isolated.err) || exit $?
+  db=$(find /tmp/${R}_iso -name '*.db' -print -quit)
+  python3 scripts/prof_summary.py "$db" gpurun_out/${R}_isolated_kernels.md > /dev/null || exit $?
   R=${R} ARGS="--steps 1 --warmup 1 --batch 48 --no-cpu-baseline" bash scripts/pmc_passes.sh || exit $?
   python3 scripts/pmc_table.py gpurun_out/${R} gpurun_out/${R}_pmc.json > gpurun_out/${R}_pmc_table.md || exit $?
 else

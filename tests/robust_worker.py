@@ -1,6 +1,6 @@
 """Child process of tests/test_gpu_robustness.py (a fresh device context per
 run). usage: robust_worker.py cache <dir> | concurrent | exit | queues |
-stmts_hbm <GB>"""
+stmts_hbm <GB> | stmts_oom"""
 import json
 import os
 import sys
@@ -124,6 +124,33 @@ def stmts_hbm(foreign_gb):
           flush=True)
 
 
+def stmts_oom():
+    """bpg_prove_statements with three device threads while the parent's
+    BPG_TEST_INJECT_OOM makes the first proof to reach that IPP round throw
+    hipErrorOutOfMemory half way through gpu_prove_lockstep: that device
+    thread hands its statements back, frees its workspace and retires
+    (ADVICE r5), the others prove them, and every proof must still equal
+    the statement's own sequential c_prove."""
+    import workloads as W
+    bpg = W._bpg()
+    sts = [W.config2(4100 + k) for k in range(12)]
+    seeds = [500 + k for k in range(len(sts))]
+    bpg.set_statements_layout(3, 2)
+    err = None
+    try:
+        outs = bpg.prove_statements("oom", sts, 6, seeds=seeds)
+    except bpg.BpgError as e:
+        outs, err = [], str(e)
+    st = bpg.last_statements_stats()
+    same = []
+    for k, (s, seed) in enumerate(zip(sts, seeds)):
+        if k < len(outs):
+            bpg.set_seed(seed)
+            same.append(outs[k] is not None and outs[k] == bpg.prove("oom", *s))
+    print(json.dumps({"proved": sum(o is not None for o in outs), "count": len(sts), "error": err,
+                      "stats": st, "same": same}), flush=True)
+
+
 def hog_bytes(gb, free):
     return int(min(gb * 1e9, free - 40e9))
 
@@ -131,6 +158,9 @@ def hog_bytes(gb, free):
 if __name__ == "__main__":
     if sys.argv[1] == "stmts_hbm":
         stmts_hbm(float(sys.argv[2]))
+        sys.exit(0)
+    if sys.argv[1] == "stmts_oom":
+        stmts_oom()
         sys.exit(0)
     if sys.argv[1] == "queues":
         queues()

@@ -133,3 +133,22 @@ def test_statements_layout_next_to_foreign_allocation(bpg):
     assert out["error"] is None, json.dumps(out)[:2000]
     assert out["proved"] == out["count"] and out["verified_last"], json.dumps(out)[:2000]
     assert 1 <= st["consumers"] <= 12, st
+    # the admission's estimate holds: no device thread had to retire on an
+    # out-of-memory error
+    assert st["oom_retired"] == 0, st
+    # and no device thread's workspace outgrew the estimate it was admitted by
+    assert 0 < st["ws_gb_max"] <= st["est_gb_per_device_thread"], st
+
+
+def test_statements_device_thread_retires_on_oom():
+    """a device thread whose proof fails with hipErrorOutOfMemory
+    half way through (injected at IPP round 3 by BPG_TEST_INJECT_OOM) retires
+    and hands its statements back; the other device threads prove them, and
+    the bytes equal sequential proving (a half-finished lockstep step leaves
+    the prepared statements and their TranscriptRng draws untouched)."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", BPG_TEST_INJECT_OOM="3")
+    out = run("stmts_oom", env=env)
+    st = out["stats"]
+    assert out["error"] is None, json.dumps(out)[:2000]
+    assert st["oom_retired"] == 1 and st["consumers"] == 3, st
+    assert out["proved"] == out["count"] and all(out["same"]) and len(out["same"]) == out["count"], out

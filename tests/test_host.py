@@ -145,7 +145,7 @@ SCRATCH_FREE = ["k_msm_digits", "k_rs_hist", "k_rs_colscan", "k_rs_scatter", "k_
                 "k_ipp_comb_fold", "k_ipp_fold3", "k_cached_to_niels", "k_flatten_short", "k_flatten_long",
                 "k_flatten_range", "k_gather_scalars", "k_gather_niels", "k_from_mont", "k_lr_build", "k_lr_eval",
                 "k_pow_table", "k_pow_expand", "k_wide_reduce", "k_fill_scalars", "k_pedersen", "k_decompress",
-                "k_verify_gh", "k_niels_neg", "k_eq_gather"]
+                "k_verify_gh", "k_niels_neg", "k_eq_gather", "k_gen_sum", "k_verify_tables"]
 
 
 @pytest.mark.parametrize("name", SCRATCH_FREE)
