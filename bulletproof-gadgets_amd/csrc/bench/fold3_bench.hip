@@ -68,10 +68,13 @@ int main(int argc, char **argv) {
     const size_t tb = ipp_fold3_table_bytes(hq, 1);
     void *tab; BPG_HIP(hipMalloc(&tab, tb));
     hipEvent_t e0, e1; BPG_HIP(hipEventCreate(&e0)); BPG_HIP(hipEventCreate(&e1));
-    launch_ipp_fold3(Gc, Hc, MSM_CACHED, hq, 1, rstart, coef, Go, Ho, tab, tb, stage3, st);
+    const void *gin[1] = {Gc}, *hin[1] = {Hc};
+    PtD *gout[1] = {Go}, *hout[1] = {Ho};
+    const ScD (*cp[1])[COMB_MAXRANGE][7] = {coef};
+    launch_ipp_fold3(gin, hin, MSM_CACHED, hq, 1, rstart, cp, gout, hout, 1, tab, tb, stage3, st);
     BPG_HIP(hipStreamSynchronize(st));
     BPG_HIP(hipEventRecord(e0, st));
-    for (int k = 0; k < reps; k++) launch_ipp_fold3(Gc, Hc, MSM_CACHED, hq, 1, rstart, coef, Go, Ho, tab, tb, stage3, st);
+    for (int k = 0; k < reps; k++) launch_ipp_fold3(gin, hin, MSM_CACHED, hq, 1, rstart, cp, gout, hout, 1, tab, tb, stage3, st);
     BPG_HIP(hipEventRecord(e1, st));
     BPG_HIP(hipEventSynchronize(e1));
     float ms;

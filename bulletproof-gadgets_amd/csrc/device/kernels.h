@@ -162,6 +162,34 @@ void launch_wide_reduce(const uint8_t *wide, uint32_t count, uint32_t stride, ui
 void launch_pow_table(const ScD *base2, uint64_t start, uint32_t count, ScD *out, hipStream_t st);
 // out[i] = lo[i & 1023] * hi[i >> 10] * mult (Montgomery)
 void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD mult, ScD *out, hipStream_t st);
+// The power tables of a lockstep step in ONE launch (blockIdx.y = proof,
+// blockIdx.z = base): lo[p][j][i] = mont(base^i), i < 1024, and
+// hi[p][j][i] = mont(base^(1024 i)), i < nhi[p][j], from the Montgomery
+// scalars base^(2^b) at b2[p] + 80 j + b and (base^1024)^(2^b) at
+// b2[p] + 80 j + 40 + b (b < 40) that the host wrote to pinned memory: the
+// kernel reads them through its device view, so no upload copy is launched.
+struct PowBatch {
+    const ScD *b2[4];
+    ScD *lo[4][3], *hi[4][3];
+    uint32_t nhi[4][3];
+};
+void launch_pow_tables(const PowBatch &A, int P, int nbase, hipStream_t st);
+// out[p][j][i] = lo[p][j][i & 1023] * hi[p][j][i >> 10] * mult[p][j] for
+// i < count (Montgomery), j < nvec, every proof's vectors in one launch
+struct PowExpandBatch {
+    const ScD *lo[4][2], *hi[4][2];
+    ScD *out[4][2];
+    ScD mult[4][2];
+};
+void launch_pow_expand_batch(const PowExpandBatch &A, int P, int nvec, uint32_t count, hipStream_t st);
+// wide_reduce of the 2 P draw halves of a lockstep step in one launch:
+// out[q][j] = draw j * stride + offset of wide[q] (q = 2 p + half)
+struct WideBatch {
+    const uint8_t *wide[8];
+    ScD *out[8];
+};
+void launch_wide_reduce_batch(const WideBatch &A, int nq, uint32_t count, uint32_t stride, uint32_t offset,
+                              hipStream_t st);
 // flattened_constraints: columns in CSC form; out[col] = sgn * sum coeff * z^(q+1)
 struct CscDev {
     const uint32_t *col_ptr;   // ncol + 1
@@ -284,11 +312,14 @@ void launch_ipp_prep(const PrepBatch &B, int kind, int P, hipStream_t st);
 // Three-round Straus fold from level k (NielsD at level 0, else PtD):
 // out_i = P_i + sum_{t=1..7} c_t P_{i + t hq}, i < hq; coef[v][r][t-1] canonical
 // for lanes [rstart[r], rstart[r+1]). `tab`: odd-multiple tables,
-// ipp_fold3_table_bytes(hq, nrange) bytes.
+// ipp_fold3_table_bytes(hq, nrange) bytes per proof.
 size_t ipp_fold3_table_bytes(uint32_t hq, uint32_t nrange);
-void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq, uint32_t nrange,
-                      const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][7], PtD *Gout, PtD *Hout,
-                      void *tab, size_t tab_bytes, ArgStage &stage, hipStream_t st);
+// P (<= 4) proofs of a lockstep step in one launch: proof p folds Gin[p],
+// Hin[p] into Gout[p], Hout[p] with coef[p]; the same hq and lane ranges for
+// all of them; `tab` holds P x ipp_fold3_table_bytes(hq, nrange).
+void launch_ipp_fold3(const void *const *Gin, const void *const *Hin, int in_fmt, uint32_t hq, uint32_t nrange,
+                      const uint32_t *rstart, const ScD (*const *coef)[COMB_MAXRANGE][7], PtD *const *Gout,
+                      PtD *const *Hout, int P, void *tab, size_t tab_bytes, ArgStage &stage, hipStream_t st);
 // IPP tail (DESIGN.md "IPP tail without folds"): below a few thousand lanes
 // the generators stay at the last materialised level (M points each) with a
 // per-point weight w_j (Montgomery form), so the round-k base i is
@@ -308,6 +339,8 @@ void launch_verify_gh(const ScD *w, const ScD *yipm, const ScD *u2m, ScD allinv,
                       ScD xm, ScD am, ScD bm, ScD um, ScD *tables, ScD *out, ScD *ynwR, ScD *acc, ScD rho_mont,
                       bool first, const int *ok, hipStream_t st);
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st);
+// dst[q][i] = val for q < nq, i < count, in one launch (the IPP tail weights)
+void launch_fill_scalars_batch(ScD *const *dst, int nq, ScD val, uint32_t count, hipStream_t st);
 // sharded prover: dst[j] = src[j * stride + offset]
 void launch_gather_scalars(const ScD *src, uint32_t count, uint32_t stride, uint32_t offset, ScD *dst, hipStream_t st);
 // A_I1's split scalars: out = aL[eqI[0..nE)] | aL[dfI[0..nD)] | aR[dfI[0..nD)]

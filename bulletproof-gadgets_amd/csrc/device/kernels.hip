@@ -922,12 +922,34 @@ DEVI void ge_add_mem(ge &r, const ge &p, const ge *q) {
 // registers, and under the bench's concurrency waited ~10x its isolated time
 // for a SIMD with that much room, profiles/r03w_pmc_table.md).
 DEVI uint32_t row_perm(uint32_t row, uint32_t nmsm, uint32_t W) { return (row % nmsm) * W + row / nmsm; }
+// FUSED (rows of at most 256 segments, the small jobs of the IPP tail):
+// thread t first sums its own bucket segment t of the row, as k_bucket_seg
+// does, into the same segA / segT slots it reads back below, so the job
+// needs no k_bucket_seg launch (round 6).
+template <bool FUSED>
 __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restrict__ segA, ge *__restrict__ segT,
                                                     uint32_t nseg, int lgL, uint32_t nmsm, uint32_t W,
-                                                    ge *__restrict__ rows_out) {
+                                                    ge *__restrict__ rows_out, const ge *__restrict__ buckets,
+                                                    const uint8_t *__restrict__ bflag, uint32_t half,
+                                                    uint32_t seglen) {
     __shared__ ge sh[256];
     const uint32_t row = blockIdx.x, t = threadIdx.x;
     WAVE_PRIO(BPG_LAT_PRIO);
+    if constexpr (FUSED) {
+        if (t < nseg) {
+            const size_t b0 = (size_t)row * half + (size_t)t * seglen;
+            ge run, acc, p;
+            bucket_load(run, buckets, bflag, b0 + seglen - 1);
+            acc = run;
+            for (int b = (int)seglen - 2; b >= 0; b--) {
+                bucket_load(p, buckets, bflag, b0 + b);
+                ge_add(run, run, p);
+                ge_add(acc, acc, run);
+            }
+            ge_store(const_cast<ge *>(segA) + (size_t)row * nseg + t, acc);
+            ge_store(segT + (size_t)row * nseg + t, run);
+        }
+    }
     const uint32_t K = (nseg + 255) / 256;
     int lgK = 0;
     while ((1u << lgK) < K) lgK++;
@@ -1350,12 +1372,19 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     ge *rows_out = rows_direct ? reinterpret_cast<ge *>(rows_direct) : AS_GE(rows_dev_.p);
     uint32_t nthr = (uint32_t)p.rows * p.nseg_per_row;
     ge *segA = AS_GE(segacc_.p), *segT = segA + (size_t)p.rows * p.nseg_per_row;
-    hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
-                       (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, segA, segT);
     int lgL = 0;
     while ((1 << lgL) < p.seglen) lgL++;
-    hipLaunchKernelGGL(k_row_reduce, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, segT,
-                       (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out));
+    if (p.nseg_per_row <= 256) {   // one segment per row thread: summed by the row kernel itself
+        hipLaunchKernelGGL(k_row_reduce<true>, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, segT,
+                           (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out),
+                           AS_CGE(buckets_.p), (const uint8_t *)bflag, (uint32_t)p.half, (uint32_t)p.seglen);
+    } else {
+        hipLaunchKernelGGL(k_bucket_seg, dim3(nblk(nthr, 64)), dim3(64), 0, st_, AS_CGE(buckets_.p), bflag,
+                           (uint32_t)p.rows, (uint32_t)p.half, (uint32_t)p.seglen, (uint32_t)p.nseg_per_row, segA, segT);
+        hipLaunchKernelGGL(k_row_reduce<false>, dim3(p.rows), dim3(256), 0, st_, (const ge *)segA, segT,
+                           (uint32_t)p.nseg_per_row, lgL, (uint32_t)nmsm, (uint32_t)p.W, AS_GE(rows_out),
+                           (const ge *)nullptr, (const uint8_t *)nullptr, 0u, 0u);
+    }
     BPG_HIP(hipGetLastError());
     if (!rows_direct)
         BPG_HIP(hipMemcpyAsync(rows_host, rows_dev_.p, (size_t)p.rows * sizeof(ge), hipMemcpyDeviceToHost, st_));
@@ -1432,6 +1461,78 @@ void launch_pow_expand(const ScD *lo, const ScD *hi, uint32_t count, ScD mult, S
     if (!count) return;
     hipLaunchKernelGGL(k_pow_expand, dim3(nblk(count, 256)), dim3(256), 0, st, AS_CSC(lo), AS_CSC(hi), count,
                        *reinterpret_cast<sc *>(&mult), AS_SC(out));
+    BPG_HIP(hipGetLastError());
+}
+
+// Batched power tables (PowBatch): block (x, p, j) covers entries
+// [256 x, 256 x + 256) of the concatenation lo (1024) | hi (nhi) of base j of
+// proof p. The block's 40 doubling powers come from pinned host memory (the
+// host wrote them before the launch; fine-grained, read once per block into
+// LDS, one 32-B scalar per thread of the first 40).
+__global__ __launch_bounds__(256) void k_pow_tables(PowBatch A) {
+    WAVE_PRIO(BPG_MISC_PRIO);
+    const uint32_t p = blockIdx.y, j = blockIdx.z;
+    const uint32_t i0 = blockIdx.x * 256, nhi = A.nhi[p][j];
+    if (i0 >= 1024 + nhi) return;
+    const bool hi = i0 >= 1024;
+    __shared__ sc b2[40];
+    if (threadIdx.x < 40) sc_load(b2[threadIdx.x], AS_CSC(A.b2[p]) + 80 * j + (hi ? 40 : 0) + threadIdx.x);
+    __syncthreads();
+    const uint32_t i = i0 + threadIdx.x;
+    if (i >= 1024 + nhi) return;
+    uint64_t e = hi ? i - 1024 : i;
+    sc acc;   // mont(1) = R mod l
+    acc.v[0] = 0x8d98951du; acc.v[1] = 0xd6ec3174u; acc.v[2] = 0x737dcf70u; acc.v[3] = 0xc6ef5bf4u;
+    acc.v[4] = 0xfffffffeu; acc.v[5] = 0xffffffffu; acc.v[6] = 0xffffffffu; acc.v[7] = 0x0fffffffu;
+    for (int b = 0; b < 40 && e; b++, e >>= 1)
+        if (e & 1) { sc t = b2[b]; mm(acc, acc, t); }
+    sc_store(hi ? AS_SC(A.hi[p][j]) + (i - 1024) : AS_SC(A.lo[p][j]) + i, acc);
+}
+void launch_pow_tables(const PowBatch &A, int P, int nbase, hipStream_t st) {
+    if (P < 1 || P > 4 || nbase < 1 || nbase > 3) throw HipError(hipErrorInvalidValue, "pow tables", __FILE__, __LINE__);
+    uint32_t mx = 0;
+    for (int p = 0; p < P; p++)
+        for (int j = 0; j < nbase; j++) mx = std::max(mx, A.nhi[p][j]);
+    hipLaunchKernelGGL(k_pow_tables, dim3(nblk(1024 + mx, 256), P, nbase), dim3(256), 0, st, A);
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_pow_expand_batch(PowExpandBatch A, uint32_t count) {
+    WAVE_PRIO(BPG_MISC_PRIO);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y, j = blockIdx.z;
+    if (i >= count) return;
+    sc a, b, r, m = *reinterpret_cast<const sc *>(&A.mult[p][j]);
+    sc_load(a, AS_CSC(A.lo[p][j]) + (i & 1023)); sc_load(b, AS_CSC(A.hi[p][j]) + (i >> 10));
+    mm(r, a, b);
+    mm(r, r, m);
+    sc_store(AS_SC(A.out[p][j]) + i, r);
+}
+void launch_pow_expand_batch(const PowExpandBatch &A, int P, int nvec, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    if (P < 1 || P > 4 || nvec < 1 || nvec > 2) throw HipError(hipErrorInvalidValue, "pow expand", __FILE__, __LINE__);
+    hipLaunchKernelGGL(k_pow_expand_batch, dim3(nblk(count, 256), P, nvec), dim3(256), 0, st, A, count);
+    BPG_HIP(hipGetLastError());
+}
+__global__ void k_wide_reduce_batch(WideBatch A, uint32_t count, uint32_t stride, uint32_t offset) {
+    WAVE_PRIO(BPG_MISC_PRIO);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, q = blockIdx.y;
+    if (i >= count) return;
+    const uint4 *w = reinterpret_cast<const uint4 *>(A.wide[q] + 64 * ((size_t)i * stride + offset));
+    uint4 q0 = w[0], q1 = w[1], q2 = w[2], q3 = w[3];
+    sc lo, hi, r2, a, b;
+    lo.v[0] = q0.x; lo.v[1] = q0.y; lo.v[2] = q0.z; lo.v[3] = q0.w; lo.v[4] = q1.x; lo.v[5] = q1.y; lo.v[6] = q1.z; lo.v[7] = q1.w;
+    hi.v[0] = q2.x; hi.v[1] = q2.y; hi.v[2] = q2.z; hi.v[3] = q2.w; hi.v[4] = q3.x; hi.v[5] = q3.y; hi.v[6] = q3.z; hi.v[7] = q3.w;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r2.v[k] = SC_R2[k];
+    sc_reduce(a, lo);
+    sc_montmul(b, hi, r2);
+    sc_add(a, a, b);
+    sc_store(AS_SC(A.out[q]) + i, a);
+}
+void launch_wide_reduce_batch(const WideBatch &A, int nq, uint32_t count, uint32_t stride, uint32_t offset,
+                              hipStream_t st) {
+    if (!count) return;
+    if (nq < 1 || nq > 8) throw HipError(hipErrorInvalidValue, "wide reduce batch", __FILE__, __LINE__);
+    hipLaunchKernelGGL(k_wide_reduce_batch, dim3(nblk(count, 256), nq), dim3(256), 0, st, A, count, stride, offset);
     BPG_HIP(hipGetLastError());
 }
 
@@ -2151,19 +2252,23 @@ void launch_ipp_fold2(const void *Gin, const void *Hin, int in_fmt, uint32_t h1,
 // NAF width 4 (odd multiples P..7P); width 5 measured no better (fewer
 // additions, twice the table, profiles/r02w_ab_fold3_w5.txt)
 static constexpr int BPG_FOLD3_WNAF = 4;
-#define FOLDN_MAXSEG (2 * COMB_MAXRANGE)
+// segments: (proof, vector, lane range); every proof of a lockstep step in
+// one launch (round 6: one launch and one argument upload per step instead
+// of one of each per proof)
+#define FOLDN_MAXSEG (2 * COMB_MAXRANGE * 4)
 #define FOLDN_MAXOPS 640
 static constexpr int FOLDN_K = 7;
 static constexpr int FOLDN_MULT = 1 << (BPG_FOLD3_WNAF - 2);           // odd multiples per point
 static constexpr uint32_t FOLDN_TABW = FOLDN_K * FOLDN_MULT * 40 * 64;  // table words per block
 struct FoldNArgs {
-    const void *in[2];
-    gec *out[2];
     uint32_t *tab;             // blocks x FOLDN_TABW words
     uint32_t hq, nseg;
-    uint32_t start[FOLDN_MAXSEG], end[FOLDN_MAXSEG], blk0[FOLDN_MAXSEG + 1], vec[FOLDN_MAXSEG];
+    const void *in[FOLDN_MAXSEG];   // the segment's level (its proof's G or H)
+    gec *out[FOLDN_MAXSEG];
+    uint32_t start[FOLDN_MAXSEG], end[FOLDN_MAXSEG], blk0[FOLDN_MAXSEG + 1];
     uint32_t nops[FOLDN_MAXSEG], tail[FOLDN_MAXSEG];
     // op: gap (8 bits) | point t - 1 << 8 (3 bits) | (m >> 1) << 11 (3 bits) | neg << 15
+    // (uploaded up to the last segment's list only)
     uint16_t ops[FOLDN_MAXSEG][FOLDN_MAXOPS];
 };
 DEVI void foldn_put(uint32_t *tb, const gec &c) {
@@ -2214,7 +2319,7 @@ DEVI const uint32_t *foldn_entry(const uint32_t *tb, uint32_t op) {
 }
 // The Straus chain over a built table, then + P_i, out as a cached point.
 template <class P>
-DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i, uint32_t v, const uint32_t *tb) {
+DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i, const uint32_t *tb) {
     const uint32_t nops = A.nops[sg];
     const uint16_t *ops = A.ops[sg];
     ge acc;
@@ -2254,7 +2359,7 @@ DEVI void foldn_chain(const FoldNArgs &A, uint32_t sg, const P *Pin, uint32_t i,
     ge_add_c(r, acc, P0);
     gec out;
     ge_to_cached(out, r);
-    gec_store(A.out[v] + i, out);
+    gec_store(A.out[sg] + i, out);
 }
 DEVI bool foldn_lane(const FoldNArgs &A, uint32_t &sg, uint32_t &i) {
     const uint32_t b = blockIdx.x;
@@ -2269,27 +2374,27 @@ __global__ __launch_bounds__(64, FOLD3_WAVES) void k_ipp_fold3(const FoldNArgs *
     const FoldNArgs &A = *Ap;
     uint32_t sg, i;
     if (!foldn_lane(A, sg, i)) return;
-    const uint32_t v = A.vec[sg];
-    const P *Pin = reinterpret_cast<const P *>(A.in[v]);
+    const P *Pin = reinterpret_cast<const P *>(A.in[sg]);
     if (A.nops[sg] == 0) {
         gec P0;
         load_as_cached(P0, Pin + i);
-        gec_store(A.out[v] + i, P0);
+        gec_store(A.out[sg] + i, P0);
         return;
     }
     uint32_t *tb = A.tab + (size_t)blockIdx.x * FOLDN_TABW + threadIdx.x;
     foldn_build(Pin, A.hq, i, tb);
-    foldn_chain(A, sg, Pin, i, v, tb);
+    foldn_chain(A, sg, Pin, i, tb);
 }
 size_t ipp_fold3_table_bytes(uint32_t hq, uint32_t nrange) {
-    // blocks: per vector and range, whole 64-lane blocks
+    // blocks: per vector and range, whole 64-lane blocks (one proof's)
     return ((size_t)2 * (hq / 64 + nrange + 1)) * FOLDN_TABW * 4;
 }
-void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq, uint32_t nrange,
-                      const uint32_t *rstart, const ScD (*coef)[COMB_MAXRANGE][7], PtD *Gout, PtD *Hout,
-                      void *tab, size_t tab_bytes, ArgStage &stage, hipStream_t st) {
+void launch_ipp_fold3(const void *const *Gin, const void *const *Hin, int in_fmt, uint32_t hq, uint32_t nrange,
+                      const uint32_t *rstart, const ScD (*const *coef)[COMB_MAXRANGE][7], PtD *const *Gout,
+                      PtD *const *Hout, int P, void *tab, size_t tab_bytes, ArgStage &stage, hipStream_t st) {
     if (!hq) return;
     if (nrange < 1 || nrange > COMB_MAXRANGE) throw HipError(hipErrorInvalidValue, "fold3 ranges", __FILE__, __LINE__);
+    if (P < 1 || P > 4) throw HipError(hipErrorInvalidValue, "fold3 proofs", __FILE__, __LINE__);
     if (!stage.dev) {
         BPG_HIP(hipMalloc(&stage.dev, sizeof(FoldNArgs)));
         BPG_HIP(hipHostMalloc(&stage.host, sizeof(FoldNArgs), hipHostMallocDefault));
@@ -2298,25 +2403,26 @@ void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq,
         event_wait(stage.copied);
     }
     FoldNArgs &A = *reinterpret_cast<FoldNArgs *>(stage.host);
-    A.in[0] = Gin; A.in[1] = Hin;
-    A.out[0] = AS_GEC(Gout); A.out[1] = AS_GEC(Hout);
     A.tab = reinterpret_cast<uint32_t *>(tab);
     A.hq = hq;
     A.nseg = 0;
     uint32_t blocks = 0;
     double fem = 0;
     constexpr int WN = BPG_FOLD3_WNAF;
+    for (int p = 0; p < P; p++)
     for (uint32_t v = 0; v < 2; v++)
         for (uint32_t r = 0; r < nrange; r++) {
             const uint32_t lo = rstart[r], hi = r + 1 < nrange ? rstart[r + 1] : hq;
             if (hi <= lo) continue;
             const uint32_t s = A.nseg++;
-            A.start[s] = lo; A.end[s] = hi; A.vec[s] = v; A.blk0[s] = blocks;
+            A.start[s] = lo; A.end[s] = hi; A.blk0[s] = blocks;
+            A.in[s] = v ? Hin[p] : Gin[p];
+            A.out[s] = AS_GEC(v ? Hout[p] : Gout[p]);
             blocks += nblk(hi - lo, 64);
             int8_t d[FOLDN_K][264];
             int len[FOLDN_K], top = -1;
             for (int t = 0; t < FOLDN_K; t++) {
-                len[t] = wnaf_digits(coef[v][r][t], WN, d[t]);
+                len[t] = wnaf_digits(coef[p][v][r][t], WN, d[t]);
                 top = std::max(top, len[t] - 1);
             }
             uint32_t n = 0, dbl = 0;
@@ -2341,10 +2447,12 @@ void launch_ipp_fold3(const void *Gin, const void *Hin, int in_fmt, uint32_t hq,
     A.blk0[A.nseg] = blocks;
     if (!blocks) return;
     if ((size_t)blocks * FOLDN_TABW * 4 > tab_bytes) throw HipError(hipErrorInvalidValue, "fold3 table", __FILE__, __LINE__);
-    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(FoldNArgs), hipMemcpyHostToDevice, st));
+    // the used segments' op lists only (ops is the struct's last member)
+    const size_t bytes = offsetof(FoldNArgs, ops) + (size_t)A.nseg * sizeof(A.ops[0]);
+    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, bytes, hipMemcpyHostToDevice, st));
     BPG_HIP(hipEventRecord(stage.copied, st));
-    // reads 8 points, writes 1 per output lane, G and H (SURVEY §8d accounting)
-    ProfScope ps(in_fmt == MSM_NIELS ? "ipp_fold3" : "ipp_fold3_cached", 2.0 * hq * 9 * 64, fem);   // one label per kernel
+    // reads 8 points, writes 1 per output lane, G and H, every proof (SURVEY §8d accounting)
+    ProfScope ps(in_fmt == MSM_NIELS ? "ipp_fold3" : "ipp_fold3_cached", 2.0 * P * hq * 9 * 64, fem);   // one label per kernel
     const FoldNArgs *dA = reinterpret_cast<const FoldNArgs *>(stage.dev);
     if (in_fmt == MSM_NIELS) hipLaunchKernelGGL(k_ipp_fold3<gen>, dim3(blocks), dim3(64), 0, st, dA);
     else hipLaunchKernelGGL(k_ipp_fold3<gec>, dim3(blocks), dim3(64), 0, st, dA);
@@ -2449,9 +2557,11 @@ void launch_comb_build(const NielsD *gens, uint32_t j0, uint32_t ntab, void *tab
 //   out_i = P_i + sum_{t<3} c_t * P_{i + (t+1) h1}
 // with per-lane-range coefficient digits (signed radix 2^COMB_BITS, LSB
 // first); no doublings: every nonzero digit is one table read and one 7M madd.
-__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restrict__ Ap) {
+// The arguments (3.2 KB with the digit lists) travel by value in the
+// kernel-argument segment: no staged upload, i.e. no copy launch per fold
+// (round 6; they were a __amd_rocclr_copyBuffer dispatch before each fold)
+__global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs A) {
     WAVE_PRIO(BPG_COMB_PRIO);
-    const CombArgs &A = *Ap;
     const uint32_t nb = (A.h1 + 63) / 64;
     const uint32_t v = blockIdx.x >= nb ? 1 : 0;
     const uint32_t i = (blockIdx.x - v * nb) * 64 + threadIdx.x;
@@ -2494,16 +2604,8 @@ __global__ __launch_bounds__(64, 2) void k_ipp_comb_fold(const CombArgs *__restr
 }
 void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st) {
     if (!args.h1) return;
-    if (!stage.dev) {
-        BPG_HIP(hipMalloc(&stage.dev, sizeof(CombArgs)));
-        BPG_HIP(hipHostMalloc(&stage.host, sizeof(CombArgs), hipHostMallocDefault));
-        BPG_HIP(hipEventCreateWithFlags(&stage.copied, hipEventBlockingSync | hipEventDisableTiming));
-    } else {
-        event_wait(stage.copied);
-    }
-    memcpy(stage.host, &args, sizeof(CombArgs));
-    BPG_HIP(hipMemcpyAsync(stage.dev, stage.host, sizeof(CombArgs), hipMemcpyHostToDevice, st));
-    BPG_HIP(hipEventRecord(stage.copied, st));
+    (void)stage;
+    static_assert(sizeof(CombArgs) <= 4096, "comb fold arguments must fit the kernel-argument segment");
     const uint32_t nb = (args.h1 + 63) / 64;
     // reads 4 level-0 points, writes 1 level-2 point per lane, G and H;
     // one 7M madd per nonzero digit (+ the base term and the cached output)
@@ -2516,7 +2618,7 @@ void launch_ipp_comb_fold(const CombArgs &args, ArgStage &stage, hipStream_t st)
             fem += (double)(hi - lo) * (7.0 * (nz + 1) + 1.0);
         }
     ProfScope ps("ipp_comb_fold", 2.0 * args.h1 * (4 * 64 + 64), fem);
-    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, reinterpret_cast<const CombArgs *>(stage.dev));
+    hipLaunchKernelGGL(k_ipp_comb_fold, dim3(2 * nb), dim3(64), 0, st, args);
     BPG_HIP(hipGetLastError());
 }
 
@@ -2720,6 +2822,20 @@ __global__ void k_fill_scalars(sc *dst, sc val, uint32_t count) {
     WAVE_PRIO(BPG_MISC_PRIO);
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) sc_store(dst + i, val);
+}
+struct FillBatch { sc *dst[8]; };
+__global__ void k_fill_scalars_batch(FillBatch A, sc val, uint32_t count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) sc_store(A.dst[blockIdx.y] + i, val);
+}
+void launch_fill_scalars_batch(ScD *const *dst, int nq, ScD val, uint32_t count, hipStream_t st) {
+    if (!count) return;
+    if (nq < 1 || nq > 8) throw HipError(hipErrorInvalidValue, "fill batch", __FILE__, __LINE__);
+    FillBatch A{};
+    for (int q = 0; q < nq; q++) A.dst[q] = AS_SC(dst[q]);
+    hipLaunchKernelGGL(k_fill_scalars_batch, dim3(nblk(count, 256), nq), dim3(256), 0, st, A,
+                       *reinterpret_cast<sc *>(&val), count);
+    BPG_HIP(hipGetLastError());
 }
 void launch_fill_scalars(ScD *dst, ScD val, uint32_t count, hipStream_t st) {
     if (!count) return;

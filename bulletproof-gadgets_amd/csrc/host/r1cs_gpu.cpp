@@ -410,7 +410,7 @@ void reset_kernel_stats() { std::lock_guard<std::mutex> lk(g_prof_mu); g_prof_st
 static const size_t ROWS_HALF = 1024;   // pinned MSM row buffer: commitments [0, 1024), IPP L/R [1024, 2048)
 struct ProofBufs {
     DBuf wide, sL, sR, w, wloc, l1, r0, r1, r3, ypm, yipm, zlo, zhi, ylo, yhi, tabs, a, b, mscal, partial, Gp[2], Hp[2],
-        small, wG, wH, wconv, f3tab, eqsc;
+        small, wG, wH, wconv, f3tab, eqsc, ytab;
     ScD *small_host = nullptr;   // pinned, 4096 scalars
     ScD *small_view = nullptr;   // its device view (kernels write c_L, c_R there)
     dev::ArgStage fold_stage, comb_stage, fold2_stage, fold3_stage;
@@ -423,7 +423,7 @@ struct ProofBufs {
         if (small_host) (void)hipHostFree(small_host);
         DBuf *bufs[] = {&wide, &sL, &sR, &w, &wloc, &l1, &r0, &r1, &r3, &ypm, &yipm, &zlo, &zhi, &ylo, &yhi, &tabs,
                         &a, &b, &mscal, &partial, &Gp[0], &Gp[1], &Hp[0], &Hp[1], &small, &wG, &wH, &wconv, &f3tab,
-                        &eqsc};
+                        &eqsc, &ytab};
         for (DBuf *d : bufs) if (d->p) (void)hipFree(d->p);
     }
 };
@@ -641,7 +641,8 @@ static size_t workspace_bytes(const Workspace &ws) {
     for (const ProofBufs &B : ws.pb)
         for (const DBuf *d : {&B.wide, &B.sL, &B.sR, &B.w, &B.wloc, &B.l1, &B.r0, &B.r1, &B.r3, &B.ypm, &B.yipm,
                               &B.zlo, &B.zhi, &B.ylo, &B.yhi, &B.tabs, &B.a, &B.b, &B.mscal, &B.partial, &B.Gp[0],
-                              &B.Gp[1], &B.Hp[0], &B.Hp[1], &B.small, &B.wG, &B.wH, &B.wconv, &B.f3tab, &B.eqsc})
+                              &B.Gp[1], &B.Hp[0], &B.Hp[1], &B.small, &B.wG, &B.wH, &B.wconv, &B.f3tab, &B.eqsc,
+                              &B.ytab})
             b += d->cap;
     return b;
 }
@@ -1488,6 +1489,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
     if (!pre) {
         MsmSeg seg[MAX_LOCKSTEP][6];
         int nseg[MAX_LOCKSTEP] = {0};
+        WideBatch WB{};   // s_L, s_R of every proof: one reduction launch
+        int nwq = 0;
         for (int p = 0; p < P; p++) {
             ProofBufs &B = ws.pb[p];
             const RngBlock &rb = *rbs[p];
@@ -1502,8 +1505,9 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                 BPG_HIP(hipMemcpyAsync(B.wide.p, rb.wide, 2 * (size_t)n * 64, hipMemcpyHostToDevice, st));
                 wd = as<uint8_t>(B.wide);
             }
-            launch_wide_reduce(wd, nl, world, rank, as<ScD>(B.sL), st);
-            launch_wide_reduce(wd + 64 * (size_t)n, nl, world, rank, as<ScD>(B.sR), st);
+            WB.wide[2 * nwq] = wd; WB.out[2 * nwq] = as<ScD>(B.sL);
+            WB.wide[2 * nwq + 1] = wd + 64 * (size_t)n; WB.out[2 * nwq + 1] = as<ScD>(B.sR);
+            nwq++;
             const PreparedCS &cp = *csv[p];
             MsmSeg *sg = seg[p];
             int &ns = nseg[p];
@@ -1512,6 +1516,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             sg[ns++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
             sg[ns++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};
         }
+        if (nwq) launch_wide_reduce_batch(WB, 2 * nwq, nl, world, rank, st);
         for (int p = 0; p < P && nl; p++) {
             int ph = ws.prof_begin("msm_commit", 5.0 * nl * (64 + 32));
             pA[p] = ws.msm->enqueue(seg[p], nseg[p], 3, rowsA + ROWS_PER_PROOF * p, MSM_NIELS,
@@ -1564,22 +1569,54 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
     // vectors: powers, flattened_constraints(z), l(x)/r(x) coefficients, t(x)
     // (y^i and y^-i at this rank's lanes: (y^world)^j * y^rank)
     std::vector<Scalar> y_inv(P);
+    {
+        // y^i, y^-i (at this rank's lanes: (y^world)^j y^rank) and the z^q
+        // tables of every proof of the step: one table launch and one
+        // expansion launch, the doubling powers read from pinned memory (no
+        // upload copies; 14 launches per proof before, round 5)
+        PowBatch PT{};
+        PowExpandBatch PE{};
+        for (int p = 0; p < P; p++) {
+            ProofBufs &B = ws.pb[p];
+            const PreparedCS &cp = *csv[p];
+            y_inv[p] = sc_invert(y[p]);
+            const Scalar base[3] = {sharded ? sc_pow_u64(y[p], world) : y[p],
+                                    sharded ? sc_pow_u64(y_inv[p], world) : y_inv[p], z[p]};
+            const uint32_t cnt[3] = {Nl, Nl, cp.q + 2};
+            for (int j = 0; j < 3; j++) {
+                ScD *h = B.small_host + 80 * j;
+                Scalar cur = base[j];
+                for (int b = 0; b < 40; b++) { h[b] = mont(cur); cur = cur * cur; }
+                cur = sc_pow_u64(base[j], 1024);
+                for (int b = 0; b < 40; b++) { h[40 + b] = mont(cur); cur = cur * cur; }
+                PT.nhi[p][j] = cnt[j] / 1024 + 1;
+            }
+            // lo | hi of y in ytab, of y^-1 in ylo / yhi, of z in zlo / zhi
+            // (the flatten reads those); in the workspace, not freed per
+            // proof: a hipFree synchronises the whole device
+            B.ytab.grow((1024 + (size_t)PT.nhi[p][0]) * sizeof(ScD));
+            B.ylo.grow(1024 * sizeof(ScD)); B.yhi.grow((size_t)PT.nhi[p][1] * sizeof(ScD));
+            B.zlo.grow(1024 * sizeof(ScD)); B.zhi.grow((size_t)PT.nhi[p][2] * sizeof(ScD));
+            B.ypm.grow((size_t)Nl * sizeof(ScD));
+            B.yipm.grow((size_t)Nl * sizeof(ScD));
+            PT.b2[p] = B.small_view;
+            PT.lo[p][0] = as<ScD>(B.ytab); PT.hi[p][0] = as<ScD>(B.ytab) + 1024;
+            PT.lo[p][1] = as<ScD>(B.ylo); PT.hi[p][1] = as<ScD>(B.yhi);
+            PT.lo[p][2] = as<ScD>(B.zlo); PT.hi[p][2] = as<ScD>(B.zhi);
+            for (int j = 0; j < 2; j++) { PE.lo[p][j] = PT.lo[p][j]; PE.hi[p][j] = PT.hi[p][j]; }
+            PE.out[p][0] = as<ScD>(B.ypm); PE.out[p][1] = as<ScD>(B.yipm);
+            PE.mult[p][0] = mont(sharded ? sc_pow_u64(y[p], rank) : Scalar::one());
+            PE.mult[p][1] = mont(sharded ? sc_pow_u64(y_inv[p], rank) : Scalar::one());
+        }
+        launch_pow_tables(PT, P, 3, st);
+        launch_pow_expand_batch(PE, P, 2, Nl, st);
+    }
     for (int p = 0; p < P; p++) {
         ProofBufs &B = ws.pb[p];
         const PreparedCS &cp = *csv[p];
         CscDev csc{as<uint32_t>(const_cast<DBuf &>(cp.col_ptr)), as<uint32_t>(const_cast<DBuf &>(cp.col_row)),
                    as<ScD>(const_cast<DBuf &>(cp.col_coeff)), as<uint32_t>(const_cast<DBuf &>(cp.short_cols)),
                    as<uint32_t>(const_cast<DBuf &>(cp.long_cols)), cp.nshort, cp.nlong, cp.ncol, 3 * n};
-        y_inv[p] = sc_invert(y[p]);
-        B.ypm.grow((size_t)Nl * sizeof(ScD));
-        B.yipm.grow((size_t)Nl * sizeof(ScD));
-        pow_vector(B.small_host, B.tabs, st, 0, sharded ? sc_pow_u64(y[p], world) : y[p], Nl, B.zlo, B.zhi,
-                   as<ScD>(B.ypm), sharded ? sc_pow_u64(y[p], rank) : Scalar::one());
-        // the y^-1 tables live in the workspace: a hipFree per proof would
-        // synchronise the whole device, every other stream included
-        pow_vector(B.small_host, B.tabs, st, 2, sharded ? sc_pow_u64(y_inv[p], world) : y_inv[p], Nl, B.ylo, B.yhi,
-                   as<ScD>(B.yipm), sharded ? sc_pow_u64(y_inv[p], rank) : Scalar::one());
-        pow_vector(B.small_host, B.tabs, st, 4, z[p], cp.q + 2, B.zlo, B.zhi, nullptr);
         B.w.grow((size_t)cp.ncol * sizeof(ScD) + 64);
         int pfl = ws.prof_begin("flatten", (double)cp.ncol * 32);
         launch_flatten(csc, as<ScD>(B.zlo), as<ScD>(B.zhi), as<ScD>(B.w), st);
@@ -1737,13 +1774,14 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
         if (!tail && depth == 0 && cur >= 0 && len <= tail_len && len >= (sharded ? 2u : 4u)) {
             tail = true;
             M = len;
+            ScD *wq[2 * MAX_LOCKSTEP];
             for (int p = 0; p < P; p++) {
                 ProofBufs &B = ws.pb[p];
                 B.wG.grow((size_t)M * sizeof(ScD) + 64);
                 B.wH.grow((size_t)M * sizeof(ScD) + 64);
-                launch_fill_scalars(as<ScD>(B.wG), mont(Scalar::one()), M, st);
-                launch_fill_scalars(as<ScD>(B.wH), mont(Scalar::one()), M, st);
+                wq[2 * p] = as<ScD>(B.wG); wq[2 * p + 1] = as<ScD>(B.wH);
             }
+            launch_fill_scalars_batch(wq, 2 * P, mont(Scalar::one()), M, st);
         }
         // MSM bases: the level-0 generators (affine Niels), else Ghat/Hhat (cached)
         const int mfmt = cur < 0 ? MSM_NIELS : gfmt;
@@ -1972,10 +2010,16 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                 starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
                 if (starts.size() > COMB_MAXRANGE) throw std::runtime_error("fold3 ranges");
                 auto cls = [&](uint64_t xx, uint64_t half) { return xx < nl && xx + half >= nl ? 1 : 0; };
+                // every proof's fold in one launch (one argument upload), the
+                // tables of all its blocks in proof 0's buffer
+                ScD coefs[MAX_LOCKSTEP][2][COMB_MAXRANGE][7];
+                const ScD (*cp3[MAX_LOCKSTEP])[COMB_MAXRANGE][7];
+                const void *gin[MAX_LOCKSTEP], *hin[MAX_LOCKSTEP];
+                PtD *gout[MAX_LOCKSTEP], *hout[MAX_LOCKSTEP];
                 for (int p = 0; p < P; p++) {
                     ProofBufs &B = ws.pb[p];
                     const std::array<Scalar, 4> *rr[3] = {&rho_h[p][0], &rho_h[p][1], &rnow[p]};
-                    ScD coef[2][COMB_MAXRANGE][7];
+                    ScD (&coef)[2][COMB_MAXRANGE][7] = coefs[p];
                     for (size_t r = 0; r < starts.size(); r++) {
                         const uint64_t i = starts[r];
                         for (int t = 1; t < 8; t++) {
@@ -1990,12 +2034,15 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
                             }
                         }
                     }
-                    const size_t tb = ipp_fold3_table_bytes(hq, (uint32_t)starts.size());
-                    B.f3tab.grow(tb);
-                    launch_ipp_fold3(Gh[p], Hh[p], gfmt, hq, (uint32_t)starts.size(), starts.data(), coef,
-                                     as<PtD>(B.Gp[nxt]), as<PtD>(B.Hp[nxt]), B.f3tab.p, B.f3tab.cap, B.fold3_stage, st);
+                    cp3[p] = coef;
+                    gin[p] = Gh[p]; hin[p] = Hh[p];
+                    gout[p] = as<PtD>(B.Gp[nxt]); hout[p] = as<PtD>(B.Hp[nxt]);
                     Gh[p] = B.Gp[nxt].p; Hh[p] = B.Hp[nxt].p;
                 }
+                ProofBufs &B0 = ws.pb[0];
+                B0.f3tab.grow((size_t)P * ipp_fold3_table_bytes(hq, (uint32_t)starts.size()));
+                launch_ipp_fold3(gin, hin, gfmt, hq, (uint32_t)starts.size(), starts.data(), cp3, gout, hout, P,
+                                 B0.f3tab.p, B0.f3tab.cap, B0.fold3_stage, st);
                 cur = nxt;
                 gfmt = MSM_CACHED;
                 niels_level(h);
