@@ -559,7 +559,11 @@ def main():
     # streams' concurrency) and in the isolated leg below (one stream: the
     # kernel's own chip time)
     kernels, jobs = kernel_stats(L)
-    iso = isolated_leg(prep, L, producers, a.isolated_proofs, rank)
+    try:   # outside the timed region; a failure here must not lose the measured line
+        iso = isolated_leg(prep, L, producers, a.isolated_proofs, rank)
+    except (Exception, SystemExit) as e:
+        iso = None
+        print("bench: isolated leg failed (%s); roofline on the concurrent basis" % e, file=sys.stderr)
     roof = roofline(kernels, jobs, iso, a.steps, dt / a.steps * 1e3)
 
     total_proofs = a.steps * batch * world

@@ -1093,7 +1093,7 @@ size_t MsmEngine::job_bytes(uint64_t total, int nmsm, int fmt) {
     const int c = msm_window(total, nmsm, fmt), W = (254 + c - 1) / c;
     const uint64_t rows = (uint64_t)nmsm * W, half = 1ull << (c - 1), E0 = (uint64_t)W * total;
     const uint64_t capE = 2 * ((E0 + RBK_CHUNK - 1) / RBK_CHUNK) * RBK_BLOCK;
-    const uint64_t nseg = half / std::min<uint64_t>(half, 8);
+    const uint64_t nseg = half <= 2048 ? std::min<uint64_t>(half, 256) : half / 8;
     return 4 * grown(E0 * 4) + grown((size_t)RS_MAXBINS * (RS_MAXTILES + 1) * 4 + 256) + grown((size_t)6 * RS_MAXTILES * 4) +
            grown(capE * 4) + grown(capE * sizeof(ge)) + grown(capE + 1024) + grown((capE / 4 + 256) * sizeof(ge)) +
            grown(rows * half * sizeof(ge)) + grown(rows * half) + grown(2 * rows * nseg * sizeof(ge)) +
@@ -1224,6 +1224,11 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     // buckets of a fixed-base row take 64 per segment (8192 segments)
     const uint32_t seg_cfg = std::max<uint32_t>(8, (uint32_t)p.half / 8192);
     p.seglen = p.half < seg_cfg ? p.half : seg_cfg;
+    // rows of at most 2048 buckets (the small jobs of the IPP tail): the row
+    // kernel sums the segments itself, one per thread, so they are spread
+    // over its 256 threads (2 buckets each at c = 10) instead of leaving
+    // three quarters of the block idle
+    if (p.half <= 2048) p.seglen = std::max<uint32_t>(1, (uint32_t)p.half / 256);
     p.nseg_per_row = p.half / p.seglen;
     if (total == 0) {
         for (int r = 0; r < p.rows; r++) {

@@ -12,7 +12,7 @@ for i in $(seq 1 $N); do
   for v in $LIBS; do
     name=${v%%:*}; lib=${v#*:}
     BPG_LIB_PATH=$lib timeout -k 10 400 python3 bench.py $ARGS > gpurun_out/${T}_${name}_$i.json 2> gpurun_out/${T}_${name}_$i.err || exit $?
-    python3 -c "import json,sys; d=json.load(open('gpurun_out/${T}_${name}_$i.json')); print('%-10s run %d  %.2f M constraints/s  %.1f ms/step  latency %.1f ms' % ('$name', $i, d['value']/1e6, d['ms_per_step'], d.get('latency_ms_single_proof') or 0))" >> gpurun_out/${T}_ab.txt
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/${T}_${name}_$i.json')); g=d.get('gpu_telemetry') or {}; print('%-10s run %d  %.2f M constraints/s  %.1f ms/step  latency %.1f ms  sclk %s MHz  power %s W' % ('$name', $i, d['value']/1e6, d['ms_per_step'], d.get('latency_ms_single_proof') or 0, (g.get('sclk_mhz') or {}).get('mean'), (g.get('power_w') or {}).get('mean')))" >> gpurun_out/${T}_ab.txt
   done
 done
 cat gpurun_out/${T}_ab.txt
