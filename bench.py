@@ -94,8 +94,8 @@ def parse():
 # single kernels bracketed live (bpg name -> rocprofv3 kernel name); every
 # label brackets exactly one kernel instantiation, so a label's launch count,
 # average and bytes are that rocprof kernel's
-KERNELS = {"msm_pass1_gens": "k_rbk_pass<true, 1, true>", "msm_pass1_folded": "k_rbk_pass<true, 1, false>",
-           "msm_pass1_cached": "k_rbk_pass<true, 0, false>",
+KERNELS = {"msm_pass1_gens": "k_rbk_pass<true, 1, 2>", "msm_pass1_folded": "k_rbk_pass<true, 1, 0>",
+           "msm_pass1_cached": "k_rbk_pass<true, 0, 0>", "msm_pass1_negc": "k_rbk_pass<true, 1, 1>",
            "ipp_fold_points": "k_ipp_fold_points<gec>", "ipp_fold_points_niels": "k_ipp_fold_points<gen>",
            "ipp_fold2_niels": "k_ipp_fold2<gen, 3>",
            "ipp_comb_fold": "k_ipp_comb_fold", "ipp_fold2": "k_ipp_fold2<gec, 3>", "ipp_fold3": "k_ipp_fold3<gen>",

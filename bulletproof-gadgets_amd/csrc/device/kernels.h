@@ -95,6 +95,10 @@ struct MsmSeg {
     // point indices of the segment's scalars (scal[k] multiplies base[idx[k]],
     // idx[k] < 2^25); null: scal[k] multiplies base[k]
     const uint32_t *idx = nullptr;
+    // the bases are a generator set (or G_i + H_i): a job whose every
+    // segment says so and that gathers no negated copies runs as its own
+    // kernel instantiation (k_rbk_pass<true, 1, 2>, label msm_pass1_gens)
+    bool gen = false;
 };
 // Fixed-base generator tables (DESIGN.md "Fixed-base windows"): 20-bit
 // signed windows, 13 of them cover a canonical scalar.

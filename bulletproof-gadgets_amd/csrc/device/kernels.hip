@@ -715,13 +715,21 @@ template <bool NEGC> DEVI void msm_init_loaded(ge &acc, gec &p, bool neg) {
 // merge passes and final run sums 1 (capping them at 4 waves measured no
 // gain, profiles/r02s_ab_latwaves.txt).
 static constexpr int RBK_WAVES = 3, RBK_CWAVES = 2, RBK_LAT_WAVES = 1;
-template <bool FIRST, int FMT, bool NEGC>
+// KIND: 0 bases negated in registers (folded levels, cached bases, the
+// merge passes), 1 negative digits gather pre-negated copies (the
+// verifier's generator jobs), 2 generator jobs of the prover negated in
+// registers -- the same code as 0, a kernel of its own so that its launches
+// are one rocprof row and one bench label (round 6: gathering from G and H
+// alone, 256 MB, instead of with their negations, 512 MB, measured +0.8% at
+// a 0.5% higher clock under the chip's power limit, profiles/r06g_ab.txt)
+template <bool FIRST, int FMT, int KIND>
 __global__ __launch_bounds__(RBK_BLOCK, !FIRST ? RBK_LAT_WAVES : FMT == MSM_CACHED ? RBK_CWAVES : RBK_WAVES) void k_rbk_pass(const uint32_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         const ge *__restrict__ pin, SegTab T, uint64_t E,
                                                         uint32_t invalid, int cw, uint32_t *__restrict__ kout,
                                                         ge *__restrict__ pout, ge *__restrict__ buckets,
                                                         uint8_t *__restrict__ bflag) {
+    constexpr bool NEGC = KIND == 1;
     __shared__ uint32_t sk[RBK_CHUNK + RBK_BLOCK];
     if constexpr (!FIRST) WAVE_PRIO(BPG_LAT_PRIO);
     if constexpr (FIRST && FMT == MSM_CACHED) WAVE_PRIO(BPG_CACHED_PRIO);
@@ -937,13 +945,15 @@ __global__ __launch_bounds__(256, ROW_WAVES) void k_row_reduce(const ge *__restr
     WAVE_PRIO(BPG_LAT_PRIO);
     if constexpr (FUSED) {
         if (t < nseg) {
+            // two points live (each bucket read coordinate by coordinate
+            // into its addition), as in the row phase below: 174 VGPRs, not
+            // the 210 a third live point costs
             const size_t b0 = (size_t)row * half + (size_t)t * seglen;
-            ge run, acc, p;
+            ge run, acc;
             bucket_load(run, buckets, bflag, b0 + seglen - 1);
             acc = run;
             for (int b = (int)seglen - 2; b >= 0; b--) {
-                bucket_load(p, buckets, bflag, b0 + b);
-                ge_add(run, run, p);
+                if (bflag[b0 + b]) ge_add_mem(run, run, buckets + b0 + b);
                 ge_add(acc, acc, run);
             }
             ge_store(const_cast<ge *>(segA) + (size_t)row * nseg + t, acc);
@@ -1196,6 +1206,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
     }
     // negated copies: used when every segment of a Niels job has one
     bool negc = fmt == MSM_NIELS;
+    bool gens = fmt == MSM_NIELS;   // every segment over a generator set (MsmSeg::gen)
     const size_t psz = fmt == MSM_NIELS ? sizeof(NielsD) : sizeof(PtD);
     for (int i = 0; i < nseg; i++) {
         if (segs[i].count > MSM_LOC_MASK || (fb && (uint64_t)(Wd - 1) * wstride + segs[i].count > MSM_LOC_MASK))
@@ -1205,6 +1216,7 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         T.neg[i] = segs[i].negofs ? (const void *)((const uint8_t *)segs[i].base + segs[i].negofs * (int64_t)psz)
                                   : segs[i].base;
         negc = negc && segs[i].negofs != 0;
+        gens = gens && segs[i].gen;
         T.row0[i] = segs[i].msm;
         T.idx[i] = segs[i].idx;
         if (segs[i].idx && fb) throw HipError(hipErrorInvalidValue, "indexed fixed-base segment", __FILE__, __LINE__);
@@ -1335,29 +1347,34 @@ MsmPlan MsmEngine::enqueue(const MsmSeg *segs, int nseg, int nmsm, PtD *rows_hos
         const uint32_t nblocks = (uint32_t)std::max<uint64_t>(1, (E + RBK_CHUNK - 1) / RBK_CHUNK);
         // pass 1 consumes the job's operands: 64-B point + 32-B scalar each
         // (SURVEY §8d). One label per kernel instantiation, so a label's
-        // launches are exactly one rocprof kernel: generator jobs (Niels bases
-        // with pre-negated copies, k_rbk_pass<true, 1, true>), folded IPP
-        // levels (Niels, negated in registers, <true, 1, false>) and cached
-        // bases (<true, 0, false>).
+        // launches are exactly one rocprof kernel: the prover's generator
+        // jobs (Niels, negated in registers, k_rbk_pass<true, 1, 2>), jobs
+        // gathering pre-negated generators (<true, 1, 1>: the verifier's),
+        // folded IPP levels (Niels, negated in registers, <true, 1, 0>) and
+        // cached bases (<true, 0, 0>).
         ProfScope ps(p.passes ? nullptr
                               : (fmt == MSM_CACHED ? "msm_pass1_cached"
-                                 : negc            ? "msm_pass1_gens"
+                                 : negc            ? "msm_pass1_negc"
+                                 : gens            ? "msm_pass1_gens"
                                                    : "msm_pass1_folded"),
                      96.0 * (double)total,   // one addition per entry: 8M cached, 7M Niels;
                      // each lane's first entry is a 1M conversion
                      (fmt == MSM_CACHED ? 8.0 : 7.0) * (double)p.E0 -
                          (fmt == MSM_CACHED ? 7.0 : 6.0) * (double)((p.E0 + RBK_T - 1) / RBK_T));
         if (p.passes == 0 && fmt == MSM_NIELS && negc)
-            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, true>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, 1>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+                               pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
+        else if (p.passes == 0 && fmt == MSM_NIELS && gens)
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, 2>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
                                pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         else if (p.passes == 0 && fmt == MSM_NIELS)
-            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, false>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_NIELS, 0>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
                                pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         else if (p.passes == 0)
-            hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED, false>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
+            hipLaunchKernelGGL((k_rbk_pass<true, MSM_CACHED, 0>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin, vals,
                                pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         else
-            hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED, false>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
+            hipLaunchKernelGGL((k_rbk_pass<false, MSM_CACHED, 0>), dim3(nblocks), dim3(RBK_BLOCK), 0, st_, kin,
                                vals, pin, T, E, invalid, p.c, kout, pout, buckets, bflag);
         BPG_HIP(hipGetLastError());
         p.passes++;

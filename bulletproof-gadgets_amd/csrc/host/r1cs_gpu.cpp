@@ -1248,7 +1248,10 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
     std::shared_ptr<FbTables> fbt = (cs.world == 1 && cs.strat.fixed_base()) ? ctx.fb(gs, cs.N) : nullptr;
     const void *G0 = fbt ? (const void *)fbt->G : (const void *)gs->G;
     const void *H0 = fbt ? (const void *)fbt->H : (const void *)gs->H;
-    const int64_t gneg = fbt ? (int64_t)fbt->N : (int64_t)gs->N;
+    // generator jobs negate in registers (gather set G and H, 256 MB, not
+    // with their negated copies, 512 MB: +0.8% under the power limit,
+    // profiles/r06g_ab.txt); the fixed-base tables keep their negations
+    const int64_t gneg = fbt ? (int64_t)fbt->N : 0;
     const uint64_t gws = fbt ? 2 * (uint64_t)fbt->N : 0;
     PtD *rows = ws.rows_host, *rows_dev = ws.rows_view;
     if (nl) {
@@ -1256,6 +1259,7 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         int ns = 0;
         commit_a_segments(cs, *gs, !fbt, G0, H0, gneg, gws, ws.st, B.eqsc, sa, ns);
         sa[ns++] = {as<ScD>(const_cast<DBuf &>(cs.aO)), G0, nl, 1, gneg, gws};
+        for (int i = 0; i < ns; i++) sa[i].gen = true;
         int ph = ws.prof_begin("msm_commit", 3.0 * nl * (64 + 32));
         pre.A = ws.msm->enqueue(sa, ns, 2, rows + CommitPre::ROWS_A, MSM_NIELS, rows_dev + CommitPre::ROWS_A);
         ws.prof_end(ph);
@@ -1265,7 +1269,8 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         BPG_HIP(hipStreamWaitEvent(ws.st, drawn, 0));
         ScD *s = as<ScD>(v ? B.sR : B.sL);
         launch_wide_reduce(as<uint8_t>(B.wide) + (size_t)v * 64 * n, nl, cs.world, cs.rank, s, ws.st);
-        const MsmSeg seg = {s, v ? H0 : G0, nl, 0, gneg, gws};
+        MsmSeg seg = {s, v ? H0 : G0, nl, 0, gneg, gws};
+        seg.gen = true;
         const size_t off = v ? CommitPre::ROWS_S1 : CommitPre::ROWS_S0;
         int ph = ws.prof_begin("msm_commit", 1.0 * nl * (64 + 32));
         pre.S[v] = ws.msm->enqueue(&seg, 1, 1, rows + off, MSM_NIELS, rows_dev + off);
@@ -1479,7 +1484,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
     std::shared_ptr<FbTables> fbt = (!sharded && cs.strat.fixed_base()) ? ctx.fb(gs, N) : nullptr;
     const void *G0 = fbt ? (const void *)fbt->G : (const void *)gs->G;
     const void *H0 = fbt ? (const void *)fbt->H : (const void *)gs->H;
-    const int64_t gneg = fbt ? (int64_t)fbt->N : (int64_t)gs->N;
+    // generator jobs negate in registers (as gpu_prove: one 256 MB gather set)
+    const int64_t gneg = fbt ? (int64_t)fbt->N : 0;
     const uint64_t gws = fbt ? 2 * (uint64_t)fbt->N : 0;   // MsmSeg::wstride of their segments
     // one commitment job per proof: a P-proof commitment job would be the
     // largest of the proof and size every workspace's MSM scratch (~7 GB at
@@ -1515,6 +1521,7 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             sg[ns++] = {as<ScD>(const_cast<DBuf &>(cp.aO)), G0, nl, 1, gneg, gws};
             sg[ns++] = {as<ScD>(B.sL), G0, nl, 2, gneg, gws};
             sg[ns++] = {as<ScD>(B.sR), H0, nl, 2, gneg, gws};
+            for (int i = 0; i < ns; i++) sg[i].gen = true;
         }
         if (nwq) launch_wide_reduce_batch(WB, 2 * nwq, nl, world, rank, st);
         for (int p = 0; p < P && nl; p++) {
@@ -1874,8 +1881,8 @@ std::vector<std::vector<uint8_t>> gpu_prove_lockstep(const PreparedCS *const *cs
             }
         }
         launch_ipp_prep(PB, prep_kind, P, st);
-        if (cur < 0)   // level-0 generator segments gather from the fixed-base tables
-            for (int i = 0; i < nseg; i++) seg[i].wstride = gws;
+        if (cur < 0)   // level-0 generator segments (gathering from the fixed-base tables when on)
+            for (int i = 0; i < nseg; i++) { seg[i].wstride = gws; seg[i].gen = true; }
         int ph = ws.prof_begin("msm_ipp", P * (tail ? 2.0 * M : (4.0 * h) * (1 << depth)) * (64 + 32));
         MsmPlan pl = ws.msm->enqueue(seg, nseg, 2 * P, rowsLR, mfmt, rowsLR_dev);
         ws.prof_end(ph);
