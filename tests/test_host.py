@@ -111,9 +111,11 @@ def _kernel_resources():
 
 
 @pytest.mark.parametrize("mangled,waves", [
-    ("k_rbk_passILb1ELi1ELb1E", 3),     # MSM pass 1 over the generators (the dominant kernel)
-    ("k_rbk_passILb1ELi0ELb0E", 2),     # MSM pass 1 over folded (cached) bases
-    ("k_rbk_passILb0ELi0ELb0E", 1),     # run merges
+    ("k_rbk_passILb1ELi1ELi2E", 3),     # MSM pass 1 over the generators (the dominant kernel)
+    ("k_rbk_passILb1ELi1ELi0E", 3),     # MSM pass 1 over folded levels (affine Niels)
+    ("k_rbk_passILb1ELi1ELi1E", 3),     # MSM pass 1 gathering pre-negated generators (verifier)
+    ("k_rbk_passILb1ELi0ELi0E", 2),     # MSM pass 1 over cached bases
+    ("k_rbk_passILb0ELi0ELi0E", 1),     # run merges
     ("k_ipp_comb_fold", 2),
     ("k_ipp_fold3I3gecE", 1),
     ("k_row_reduce", 1),
