@@ -830,18 +830,23 @@ std::unique_ptr<PreparedCS> prepare_cs(const bpg_r1cs_view *cs, int device, cons
                 }
             }
         }
-        // the witness copies: wiped (the barrier keeps the memset of a live
-        // buffer) and released, not kept per thread (64 MB per worker at
-        // 2^20); the equal-lane lists derive from the witness too
+        // the witness copies (and the equal-lane lists, which derive from
+        // the witness): wiped (the barrier keeps the memset of a live
+        // buffer), and kept for the thread's next statement only up to 32 MB
+        // each, a 2^20 circuit's (several GB across a large pool
+        // otherwise). Releasing them after every statement cost the
+        // statements mode's CPU workers ~45 ms of page faults and zero fills
+        // per config-5 statement (prepare 123 vs 78 ms, profiles/r06zz_statements.json)
+        const size_t KEEP = (size_t)32 << 20;
         for (std::vector<ScD> *t : {&tL, &tmp}) {
             memset(t->data(), 0, t->size() * sizeof(ScD));
             __asm__ __volatile__("" : : "r"(t->data()) : "memory");
-            std::vector<ScD>().swap(*t);
+            if (t->capacity() * sizeof(ScD) > KEEP) std::vector<ScD>().swap(*t);
         }
         for (std::vector<uint32_t> *t : {&iE, &iD}) {
             memset(t->data(), 0, t->size() * sizeof(uint32_t));
             __asm__ __volatile__("" : : "r"(t->data()) : "memory");
-            std::vector<uint32_t>().swap(*t);
+            if (t->capacity() * sizeof(uint32_t) > KEEP) std::vector<uint32_t>().swap(*t);
         }
         P->v.resize(m); P->vb.resize(m);
         std::vector<ScD> vbd(m ? m : 1);
