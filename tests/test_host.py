@@ -216,3 +216,53 @@ def test_bench_cpu_share_detection():
     assert 1 <= n <= len(os.sched_getaffinity(0))
     q = b.cpu_quota()
     assert q is None or q > 0
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_bench_roofline_exclusive_basis():
+    """`frac` comes from the isolated (one-stream) leg's
+    average launch, the timed region's stretched average is
+    `frac_concurrent`, and `consistency` checks launches per step x the
+    average against the step (synthetic stats; no GPU)."""
+    b = _bench_module()
+    MB = 1e6
+    # label -> (launches, summed ms, algorithmic bytes, fe_mul) as kernel_stats returns
+    timed = {"msm_pass1_gens": (576 * 2, 2 * 576 * 16.0, 2 * 576 * 444 * MB, 2 * 576 * 5e8),
+             "ipp_fold3": (192, 192 * 8.0, 192 * 85 * MB, 192 * 1e9)}
+    iso = {"kernels": {"msm_pass1_gens": (96, 96 * 3.4, 96 * 444 * MB, 96 * 5e8)}, "jobs": {}, "proofs": 64,
+           "wall_s": 1.7, "consumers": 1, "lockstep": 4}
+    r = b.roofline(timed, {}, iso, 2, 6000.0)
+    assert r["kernel"] == "msm_pass1_gens" and r["basis"].startswith("exclusive")
+    assert abs(r["avg_launch_ms"] - 3.4) < 1e-9 and abs(r["avg_launch_ms_concurrent"] - 16.0) < 1e-9
+    assert abs(r["frac"] - 444 * MB / 3.4e-3 / 1e9 / 8000.0) < 1e-6
+    assert abs(r["frac_concurrent"] - 444 * MB / 16e-3 / 1e9 / 8000.0) < 1e-6
+    c = r["consistency"]
+    assert c["launches_per_step"] == 576 and c["ok"] and abs(c["launches_x_avg_ms"] - 576 * 3.4) < 0.1
+    assert c["launches_x_avg_concurrent_ms"] > c["ms_per_step"]      # the stretched basis fails the check
+    assert r["kernel_table"]["ipp_fold3"]["avg_launch_ms_isolated"] is None
+    # without the isolated leg the line says which basis it fell back to
+    r0 = b.roofline(timed, {}, None, 2, 6000.0)
+    assert r0["basis"].startswith("concurrent") and r0["frac"] == r0["frac_concurrent"]
+
+
+def test_bench_telemetry_degrades_without_device():
+    """gpu_telemetry never fails the bench: without amdsmi access (no GPU
+    here) it reports the reason and no samples."""
+    b = _bench_module()
+
+    class FakeTorch:
+        class cuda:
+            @staticmethod
+            def get_device_properties(dev):
+                raise RuntimeError("no device")
+    t = b.GpuTelemetry(FakeTorch, 0, period=0.01)
+    t.start()
+    out = t.stop()
+    assert out["samples"] == 0 and "error" in out
