@@ -1299,8 +1299,11 @@ std::vector<uint8_t> gpu_prove(const PreparedCS &cs, const uint8_t *label, size_
         bool armed = true;
         ~WipeOnError() {
             if (!armed) return;
-            (void)hipStreamSynchronize(producer_stage(device).st);
-            (void)hipStreamSynchronize(ws.st);
+            // error path only: wait for every copy that may still read the
+            // buffer (the draw copies run on this thread's producer stream),
+            // allocating nothing and throwing nothing here
+            (void)hipSetDevice(device);
+            (void)hipDeviceSynchronize();
             (void)hipGetLastError();
             memset(ws.s_host, 0, bytes);
             __asm__ __volatile__("" : : "r"(ws.s_host) : "memory");
