@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--producers", type=int, default=0,
                     help="TranscriptRng producer threads per GPU (default: one per CPU of the rank's share, at most 8)")
     ap.add_argument("--ipp-tail", type=int, default=-1,
-                    help="IPP tail threshold in lanes (bpg_ctx_set_ipp_tail; -1: the default, 4096)")
+                    help="IPP tail threshold in lanes (bpg_ctx_set_ipp_tail; -1: the default, 512)")
     ap.add_argument("--consumers", type=int, default=0,
                     help="statements mode: device threads (bpg_set_statements_layout; 0: min(5, threads / 2))")
     ap.add_argument("--stmt-lockstep", type=int, default=0,
@@ -587,7 +587,7 @@ def main():
                    "pipeline": "the K steps' proofs stream through one producer/consumer pipeline",
                    "ipp_comb_tables": {-1: "default (on)", 0: "off", 1: "on"}[a.fold_tables],
                    "msm_fixed_base_tables": {-1: "default (off)", 0: "off", 1: "on"}[a.msm_tables],
-                   "ipp_tail_lanes": a.ipp_tail if a.ipp_tail >= 0 else "default (4096)"},
+                   "ipp_tail_lanes": a.ipp_tail if a.ipp_tail >= 0 else "default (512)"},
         "host_cores_busy": round(host_busy, 2),
         # the producer/consumer pipeline of the timed batch (bpg_last_batch_stats):
         # consumer time starved of ready proofs while producers were drawing

@@ -151,7 +151,13 @@ CombTables::~CombTables() {
 }
 bool Strategy::tables() const { return fold_tables != 0; }
 bool Strategy::pairs() const { return fold_pairs != 0; }
-uint32_t Strategy::tail() const { return ipp_tail >= 0 ? (uint32_t)ipp_tail : 4096u; }
+// 512 since round 6 (4096 before): at 2^20 the level-8 triple fold (4096 ->
+// 512 lanes) replaces three tail rounds' 4-segment MSMs over 4096 lanes, and
+// the tail's nine rounds run over 512: ~170 K fewer MSM points per proof, a
+// few percent of the VALU work on a power-limited chip, +1.0% in three
+// alternating runs (profiles/r06t_ab_tail512.txt; 2048 and 8192 were noise
+// in rounds 2 and 4)
+uint32_t Strategy::tail() const { return ipp_tail >= 0 ? (uint32_t)ipp_tail : 512u; }
 int Strategy::group() const { return fold_pairs == 0 ? 1 : fold_pairs == 1 ? 2 : 3; }
 
 static std::mutex g_cache_mu;

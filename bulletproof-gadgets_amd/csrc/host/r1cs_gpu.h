@@ -68,7 +68,7 @@ struct FbTables {
     ~FbTables();
 };
 // IPP fold strategy, per context (bpg_ctx_set_fold_tables / _pairs / _ipp_tail):
-// -1 default (tables on, round triples, tail at 4096 lanes), 0 off, 1 on.
+// -1 default (tables on, round triples, tail at 512 lanes), 0 off, 1 on.
 // Proof bytes are identical under every strategy.
 struct Strategy {
     int fold_tables = -1, fold_pairs = -1;
@@ -77,7 +77,7 @@ struct Strategy {
     // consumer they crowd out of HBM (profiles/r04l_ab.txt)
     int msm_tables = -1;
     bool fixed_base() const { return msm_tables == 1; }
-    int ipp_tail = -1;   // IPP tail threshold in lanes (-1: 4096)
+    int ipp_tail = -1;   // IPP tail threshold in lanes (-1: 512)
     uint32_t tail() const;
     bool tables() const;
     bool pairs() const;

@@ -215,7 +215,7 @@ int bpg_ctx_set_fold_pairs(bpg_ctx *ctx, int mode);
 int bpg_ctx_set_msm_tables(bpg_ctx *ctx, int mode);
 /* IPP tail threshold of `ctx`'s calls: once a materialised generator level
  * has at most `lanes` points, the remaining rounds weight its points instead
- * of folding them (-1, the default: 4096). Proof bytes
+ * of folding them (-1, the default: 512). Proof bytes
  * are identical for every threshold; small values exercise the fold passes on
  * small circuits. The sharded prover must end its local rounds in the tail
  * and uses max(lanes, 8). */
